@@ -1,0 +1,254 @@
+"""Benchmark: propagation edges/sec (+ full-catalog top-K recs/sec) on MI355X.
+
+Workload (BASELINE.json north_star headline): synthetic uniform bipartite graph,
+1M users x 1M items, 100M interactions (200M directed nnz of A_hat), dim 64, 3 LightGCN
+layers. A "step" = one full 3-layer forward over the whole graph (gcn_norm cached, as the
+graph is fixed), with the layer mean fused. N GPUs: the rows are sharded over the ranks
+and the propagated embeddings are all-gathered over RCCL after every layer (strong
+scaling: the graph is fixed, value = all nnz x layers / max-over-ranks time).
+
+After the timed steps, a second phase times the masked full-catalog top-20 (e0 scores,
+-1024 exclusion of each user's train+val items) for a block of users per rank over all 1M
+items: reported as "topk" (recs/s, aggregated over ranks).
+
+Run: python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "light-graph-convolutional-recommendation-algorithm-based-on-hybrid-spreading_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F32_MFMA_PEAK_TF = 157.3    # dense fp32 MFMA (= fp32 vector) peak, same table
+
+WORKLOADS = {
+    # name: (users, items, interactions, dim, layers)
+    "c5-d64": (1_000_000, 1_000_000, 100_000_000, 64, 3),
+    "c5-d128": (1_000_000, 1_000_000, 100_000_000, 128, 3),
+    "c4": (200_000, 200_000, 20_000_000, 64, 3),
+    "c2": (6_040, 3_706, 800_167, 64, 3),
+    "tiny": (20_000, 20_000, 1_000_000, 64, 3),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def gen_graph(U, I, E, seed, dev):
+    """Exactly E unique uniform (user, item) pairs on the device; returns the symmetric
+    CSR over U+I nodes (rowptr int64, src int32) plus the sorted interaction keys."""
+    from lgcnhs.graph import _rowptr_from_sorted
+    g = torch.Generator(device=dev).manual_seed(seed)
+    keys = torch.empty(0, dtype=torch.int64, device=dev)
+    while keys.numel() < E:
+        n = int((E - keys.numel()) * 1.02) + 1024
+        u = torch.randint(0, U, (n,), device=dev, generator=g)
+        i = torch.randint(0, I, (n,), device=dev, generator=g)
+        keys = torch.unique(torch.cat([keys, u * I + i]))
+        del u, i
+    if keys.numel() > E:
+        pick = torch.randperm(keys.numel(), device=dev, generator=g)[:E]
+        keys = torch.sort(keys[pick]).values
+    users = keys // I
+    items = keys % I
+    ikeys = torch.sort(items * U + users).values
+    n = U + I
+    rows = torch.cat([users, (ikeys // U) + U])          # users then items: sorted
+    src = torch.cat([items + U, ikeys % U]).to(torch.int32)
+    del ikeys, items
+    rowptr = _rowptr_from_sorted(rows, n)
+    del rows
+    return rowptr, src, keys
+
+
+def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
+    """The oracle's PyG op sequence (index_select * w, index_add_) on the host cores over a
+    bounded sample: the first rows of the graph until ~target_nnz edges, full-size x."""
+    from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
+    rp = rowptr.cpu()
+    r_end = int(torch.searchsorted(rp, torch.tensor([target_nnz])).item())
+    r_end = max(1, min(r_end, n))
+    e_end = int(rp[r_end])
+    s = src[:e_end].cpu().to(torch.int64)
+    deg = (rp[1:r_end + 1] - rp[:r_end])
+    t = torch.repeat_interleave(torch.arange(r_end), deg)
+    ei = torch.stack([s, t])
+    full_deg = (rp[1:] - rp[:-1]).float()
+    dis = full_deg.pow(-0.5)
+    dis.masked_fill_(dis == float("inf"), 0)
+    w = dis[s] * dis[t]
+    x = torch.randn(n, dim) * 0.1
+    O.propagate(ei, w, x)  # warm-up
+    reps = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        cur = x
+        for _ in range(layers):
+            cur = O.propagate(ei, w, cur)
+        reps.append(time.perf_counter() - t0)
+    secs = sorted(reps)[1]
+    return {"value": e_end * layers / secs, "unit": "edge-layers/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"PyG op sequence (index_select*w, index_add_) over rows [0,{r_end}) = "
+                      f"{e_end} directed nnz x {layers} layers, full {n}x{dim} x, median of 3"}
+
+
+def load_traffic(workload, world):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        e = d.get(f"{workload}/n{world}")
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c5-d64", choices=sorted(WORKLOADS))
+    ap.add_argument("--topk-users", type=int, default=32768, help="users per rank for the top-K phase")
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-topk", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from lgcnhs import ops
+    from lgcnhs.dist import RowShard, ShardedPropagation
+    from lgcnhs.graph import RowSets
+
+    U, I, E, D, L = WORKLOADS[args.workload]
+    N = U + I
+    t0 = time.time()
+    rowptr, src, keys = gen_graph(U, I, E, seed=0, dev=dev)
+    nnz = int(src.numel())
+    shard = RowShard(rowptr, src, N, rank, world, dev)
+    from lgcnhs import _native as NV
+    dis = torch.empty(N, dtype=torch.float32, device=dev)
+    NV.check(NV.lib().lg_gcn_norm_f32(NV.ptr(rowptr), N, NV.ptr(dis), NV.stream_handle(dev)),
+             "gcn_norm")
+    gen = torch.Generator(device=dev).manual_seed(42)
+    e0 = torch.zeros(shard.n_pad, D, device=dev)
+    e0[:N] = torch.randn(N, D, device=dev, generator=gen) * 0.1
+    prop = ShardedPropagation(shard, dis, D, L, dev)
+    cpu_rp, cpu_src = (rowptr, src) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else (None, None)
+    del rowptr
+    if cpu_src is None:
+        del src
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {shard.r0}-{shard.r1} "
+        f"setup {time.time() - t0:.1f}s")
+
+    for _ in range(args.warmup):
+        prop.forward(e0)
+    torch.cuda.synchronize()
+    prop.events = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        prop.forward(e0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    kernel_ms = [s.elapsed_time(e) for s, e in prop.events]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    edge_layers = nnz * L * args.steps
+    value = edge_layers / elapsed
+    # algorithmic bytes per SpMM launch: nnz*(8+4d) + rows*(4+4d)
+    alg_bytes = shard.nnz * (8 + 4 * D) + shard.n_rows * (4 + 4 * D)
+    achieved = alg_bytes / avg_kernel_s / 1e9
+    traffic = load_traffic(args.workload, world)
+
+    topk = None
+    if not args.no_topk:
+        nu = min(args.topk_users, U)
+        u0 = (rank * nu) % max(1, U - nu + 1)
+        eu = e0[u0:u0 + nu].contiguous()
+        ei = e0[U:U + I].contiguous()
+        ku = keys[(keys >= u0 * I) & (keys < (u0 + nu) * I)]  # this block's positives
+        excl = RowSets.from_pairs(ku // I - u0, ku % I, nu, I, dev)
+        ops.score_topk(eu, ei, args.k, excl)  # warm-up
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        reps = 3
+        for _ in range(reps):
+            ops.score_topk(eu, ei, args.k, excl)
+        e.record()
+        torch.cuda.synchronize()
+        tk = s.elapsed_time(e) / 1e3 / reps
+        if world > 1:
+            t = torch.tensor([tk], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tk = float(t.item())
+        flops = 2.0 * nu * I * D
+        topk = {"recs_per_s": nu * world / tk, "users_per_rank": nu, "items": I, "k": args.k,
+                "ms": tk * 1e3, "tflops_per_gpu": flops / tk / 1e12,
+                "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
+                "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
+
+    cpu = None
+    if cpu_src is not None:
+        try:
+            cpu = cpu_baseline(cpu_rp, cpu_src, N, D, L)
+        except Exception as ex:  # the baseline must never hide the GPU result
+            log(f"cpu baseline failed: {ex!r}")
+    if rank == 0:
+        line = {
+            "metric": "propagation edges/sec + full-catalog top-K recs/sec, 1/2/4/8 MI355X",
+            "value": value, "unit": "edge-layers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (uniform bipartite, seed 0; e0 ~ N(0, 0.1^2))",
+            "config": {"workload": args.workload, "users": U, "items": I, "interactions": E,
+                       "directed_nnz": nnz, "dim": D, "layers": L,
+                       "parallelism": f"row-shard x{world} + RCCL all-gather per layer"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "lg_spmm_layer_f32",
+                         "avg_launch_ms": avg_kernel_s * 1e3,
+                         "alg_bytes_per_launch": alg_bytes},
+            "topk": topk,
+            "cpu_baseline": cpu,
+            "host": platform.node(),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * lgcnhs.h — C ABI of the MI355X (gfx950) hot path for LGCNHS
+ * (Light Graph Convolutional Recommendation based on Hybrid Spreading).
+ *
+ * Every entry point replaces one piece of arithmetic that the reference runs inside
+ * third-party kernels (PyG 2.6.1, torch 1.13.1, numpy 1.24.3/MKL). The reference has no
+ * FFI of its own (it is pure Python), so the "binding" a maintainer adds is the ctypes
+ * stub shown in INTEGRATION.md; the reference call site each function replaces is cited
+ * on the function.
+ *
+ * Conventions (all functions):
+ *   - Plain device pointers, sizes and a stream. No allocation, no free, no host sync:
+ *     the caller owns every buffer; work is enqueued on `stream` (a hipStream_t, NULL =
+ *     the default stream). Safe to capture into a hipGraph.
+ *   - Return LG_OK (0) or an LG_ERR_* code; lg_last_error() gives a thread-local message.
+ *     Nothing is thrown across the ABI.
+ *   - Graph rows are CSR: int64 rowptr[n_rows+1] (absolute offsets), int32 column ids,
+ *     columns ascending inside a row (the order of the reference's coalesced COO,
+ *     utils/graph.py:32-33). Node ids cover users then items (items offset by U).
+ *   - Embeddings are row-major fp32 [n, dim]; spreading matrices are row-major fp64.
+ *   - Top-K output is sorted by (value desc, index asc); unused slots hold index -1.
+ */
+#ifndef LGCNHS_H
+#define LGCNHS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *lg_stream_t; /* hipStream_t */
+
+enum lg_status {
+  LG_OK = 0,
+  LG_ERR_ARG = 1,         /* bad size / null pointer / unsupported dim or k */
+  LG_ERR_HIP = 2,         /* a HIP runtime call failed (launch error) */
+  LG_ERR_WORKSPACE = 3,   /* workspace smaller than the *_ws_bytes() answer */
+};
+
+/* ABI version of this header (bumped on any signature change). */
+#define LG_ABI_VERSION 1
+int lg_abi_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char *lg_last_error(void);
+
+/* ------------------------------------------------------------------------------------
+ * Graph format and normalisation
+ * ------------------------------------------------------------------------------------ */
+
+/* rowptr[r] = lower_bound(keys, r) for r in [0, n_rows]; `keys` = the row id of each of
+ * `nnz` entries, sorted ascending. Replaces the dense (U+I)^2 -> to_sparse_coo() round trip
+ * of utils/graph.py:22-35 (convertEdgeIndexToAdjMatrix) as the way the graph reaches the
+ * propagation kernel. */
+int lg_csr_rowptr_from_sorted(const int64_t *keys, int64_t nnz, int64_t n_rows,
+                              int64_t *rowptr, lg_stream_t stream);
+
+/* dis[n] = deg(n)^-1/2 with deg(n) = rowptr[n+1]-rowptr[n] (in-degree as a target),
+ * inf -> 0. PyG 2.6.1 gcn_norm(add_self_loops=False), called at
+ * model/LightGCN/model.py:53 and model/LightGCNOpti/model.py:65. */
+int lg_gcn_norm_f32(const int64_t *rowptr, int64_t n_nodes, float *dis,
+                    lg_stream_t stream);
+
+/* w[e] = dis[src[e]] * dis[row_offset + r] for every entry e of row r: the edge weights
+ * gcn_norm returns (model/LightGCN/model.py:53, second tuple element). Only needed by
+ * callers that ask for the weights; the propagation kernel recomputes them on the fly. */
+int lg_gcn_edge_weight_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
+                           int64_t n_rows, int64_t row_offset, float *w,
+                           lg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * LightGCN propagation: one layer of  e^{l+1} = D^-1/2 A D^-1/2 e^l  over a row range,
+ * with the layer mean of model/LightGCN/model.py:66-69 fused into the epilogue.
+ * Replaces PyG propagate (index_select + message + scatter_add,
+ * model/LightGCN/model.py:61-63,76-84) and torch.stack/mean (:66-69).
+ *
+ * For r in [0, n_rows), node g = row_offset + r:
+ *   v[g] = sum_{e in row r, s = src[e]} (dis[s] * dis[g]) * x[s]      (ascending s)
+ *   y[g] = v[g]                                   if y != NULL
+ *   acc_mode FIRST: acc[g] = x0[g] + v[g]
+ *            MID  : acc[g] = acc[g] + v[g]
+ *            LAST : out[g] = (acc[g] + v[g]) / denom
+ *            ONLY : out[g] = (x0[g] + v[g]) / denom            (a 1-layer model)
+ *            NONE : nothing
+ * x, y, x0, acc, out are [*, dim] arrays indexed by node id g (row-sharded callers pass
+ * full-size arrays and their own row range). dim in {32, 64, 128, 256}.
+ * ------------------------------------------------------------------------------------ */
+enum lg_acc_mode {
+  LG_ACC_NONE = 0,
+  LG_ACC_FIRST = 1,
+  LG_ACC_MID = 2,
+  LG_ACC_LAST = 3,
+  LG_ACC_ONLY = 4,
+};
+int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
+                      const float *x, float *y, const float *x0, float *acc, float *out,
+                      int64_t n_rows, int64_t row_offset, int32_t dim, int32_t acc_mode,
+                      float denom, lg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Full-catalog scoring with exclusion mask and top-K.
+ * Replaces  score = e0_u @ e0_i^T ; score[train|val positives] = -1024 ; topk(score, k)
+ * of model/LightGCN/recommend.py:83-114 (same code: LightGCNOpti/recommend.py:83-114,
+ * LightGCN/evaluation.py:31-51). The U x I score matrix is never materialised.
+ *
+ * score(u, i) is the fp32 fused-multiply-add chain, in this element order,
+ *   acc = 0; for s in [0, dim/4): for g in [0, 4): acc = fmaf(eu[u][g*dim/4+s], ei[i][g*dim/4+s], acc)
+ * (what v_mfma_f32_16x16x4_f32 computes), replaced by mask_value when i is in the user's
+ * exclusion row ex_col[ex_rowptr[u] .. ex_rowptr[u+1]) (sorted ascending).
+ * eu = [n_users, dim] (a sharded caller passes its own user block and the matching
+ * ex_rowptr slice), ei = [n_items, dim]. k in [1, 128]; dim in {32, 64, 128}.
+ * n_splits >= 1 splits the item range over that many workgroup sets (for small user
+ * counts); the workspace holds the partial lists.
+ * ------------------------------------------------------------------------------------ */
+size_t lg_score_topk_ws_bytes(int64_t n_users, int64_t n_items, int32_t dim, int32_t k,
+                              int32_t n_splits);
+int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
+                      int32_t dim, const int64_t *ex_rowptr, const int32_t *ex_col,
+                      float mask_value, int32_t k, int32_t n_splits, float *out_val,
+                      int64_t *out_idx, void *ws, size_t ws_bytes, lg_stream_t stream);
+
+/* Dense masked score matrix G[u][i] (same score definition and mask as above), written
+ * with leading dimension ldg. Replaces getAllocateMat's matmul + masks
+ * (model/SpreadLightGCN/model.py:74-104, model/SpreadLightGCNOpti/model.py:139-169). */
+int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
+                       int32_t dim, const int64_t *ex_rowptr, const int32_t *ex_col,
+                       float mask_value, float *G, int64_t ldg, lg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Hybrid spreading (model/SpreadMethod/model.py), fp64, from the interaction matrix A
+ * held sparse: user rows (user_rowptr/user_items) and item rows (item_rowptr/item_users).
+ * ------------------------------------------------------------------------------------ */
+
+/* gW[i][j] = sum_{v in users(i), ascending} [j in items(v)] * (1 / k_v), k_v = |items(v)|.
+ * = np.dot(A.T / k_u, A) of getSpreadingGeneralMat (model/SpreadMethod/model.py:14-27).
+ * gW is [n_items, n_items], fully written (zeros included). */
+int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                          const int64_t *user_rowptr, const int32_t *user_items,
+                          int64_t n_users, int64_t n_items, double *gW,
+                          lg_stream_t stream);
+
+/* W[i][j] = gWsrc[i][j] / den, den = k_i^(1-lambda) * k_j^lambda, den == 0 -> 1, with
+ * gWsrc = gW (transpose_gw = 0) or gW^T (transpose_gw = 1). HybridS,
+ * model/SpreadMethod/model.py:63-85 (the .T variants: SpreadMethod/recommend.py:91,101). */
+int lg_hybrid_weight_f64(const double *gW, const double *k_item, int64_t n_items,
+                         double lambda, int32_t transpose_gw, double *W,
+                         lg_stream_t stream);
+
+/* F[u][j] = sum_{i in items(u), ascending} W[i][j] : getResource's np.dot(A, W)
+ * (model/SpreadMethod/model.py:88-99) for user rows [0, n_users). */
+int lg_spread_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
+                           const double *W, int64_t n_users, int64_t n_items, double *F,
+                           int64_t ldf, lg_stream_t stream);
+
+/* Per-row top-K over dense fp64 rows F[r][0..n_cols) (leading dim ldf), optionally
+ * multiplied by the fp32 score G[r][j] (eu/ei non-NULL; same chain as lg_score_topk_f32,
+ * promoted to fp64 before the product, as numpy's G * F does:
+ * model/SpreadLightGCN/model.py:151). Exclusion rows ex_* (may be NULL):
+ *   excl_mode DROP: excluded columns are removed (argsort + filter of
+ *                   model/SpreadMethod/recommend.py:39-47);
+ *   excl_mode NONE: nothing is removed (the unfiltered ProbS/movielens branch,
+ *                   model/SpreadMethod/recommend.py:49-50).
+ * With a G factor the exclusions must be DROP (G's -1024 mask is then never observable).
+ * k in [1, 128]. Rows with fewer than k survivors are padded with index -1. */
+enum lg_excl_mode { LG_EXCL_DROP = 0, LG_EXCL_NONE = 1 };
+int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_cols,
+                     const float *eu, const float *ei, int32_t dim,
+                     const int64_t *ex_rowptr, const int32_t *ex_col, int32_t excl_mode,
+                     int32_t k, double *out_val, int64_t *out_idx, lg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LGCNHS_H */

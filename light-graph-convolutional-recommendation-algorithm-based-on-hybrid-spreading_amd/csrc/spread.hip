@@ -1,0 +1,266 @@
+// K3/K4: hybrid spreading (mass diffusion / heat conduction mix) in fp64, gfx950.
+//
+// Reference (model/SpreadMethod/model.py), all dense numpy fp64 on the host:
+//   getSpreadingGeneralMat :14-27   k_u = A.sum(1) (0 -> 1); general_W = (A.T / k_u) @ A
+//   HybridS                :63-85   k_i = A.sum(0); den = k_i^(1-l) (x) k_j^l; den==0 -> 1;
+//                                    W = general_W / den
+//   getResource            :88-99   F = A @ W
+//   recommendForAllUser    model/SpreadMethod/recommend.py:31-50: per user
+//                                    argsort(F[u])[::-1], drop train|val items, [:k]
+//   G * F                  model/SpreadLightGCN/model.py:151 (fp32 G promoted to fp64)
+//
+// A is 0/1 and sparse, so the GEMMs are replaced by sparse row sums with a deterministic
+// ascending summation order:
+//   general_W[i][j] = sum_{v in users(i)} [j in items(v)] * fl(1/k_v)   (one block per i)
+//   F[u][j]         = sum_{i in items(u)} W[i][j]                        (one block per u)
+// which cost E*avg_deg and E*I instead of 2*U*I^2 each. Top-K over the dense rows is the
+// candidate-list selection of common.h, one wave per row, 64 columns per step.
+#include "common.h"
+
+namespace lg {
+
+__global__ __launch_bounds__(256) void k_spread_general(
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_items, double *__restrict__ gW) {
+  const int64_t i = blockIdx.x;
+  double *row = gW + i * n_items;
+  for (int64_t j = threadIdx.x; j < n_items; j += blockDim.x) row[j] = 0.0;
+  __syncthreads();
+  const int64_t eb = item_rowptr[i], ee = item_rowptr[i + 1];
+  for (int64_t e = eb; e < ee; ++e) {
+    const int32_t v = item_users[e];
+    const int64_t pb = user_rowptr[v], pe = user_rowptr[v + 1];
+    // (A.T / k_u)[i][v] = 1.0 / k_v, correctly rounded; times A[v][j] = 1 is exact.
+    const double wv = 1.0 / (double)(pe - pb);
+    for (int64_t p = pb + threadIdx.x; p < pe; p += blockDim.x) row[user_items[p]] += wv;
+    __syncthreads();  // the next user may hit the same columns from other threads
+  }
+}
+
+// 32x32 tiles; the transposed source is staged through LDS for coalesced reads. The
+// tile's 32 row factors k_i^(1-l) and 32 column factors k_j^l are computed once per tile
+// (np.power(item_degrees, 1 - Lambda) / np.power(item_degrees, Lambda)).
+__global__ __launch_bounds__(256) void k_hybrid_weight(const double *__restrict__ gW,
+                                                       const double *__restrict__ k_item,
+                                                       double lambda, int64_t n, int transpose,
+                                                       double *__restrict__ W) {
+  __shared__ double tile[32][33];
+  __shared__ double alpha[32], beta[32];
+  const int64_t bi = blockIdx.y * 32, bj = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  if (threadIdx.x < 32) {
+    const int64_t i = bi + threadIdx.x;
+    alpha[threadIdx.x] = i < n ? pow(k_item[i], 1.0 - lambda) : 1.0;
+  } else if (threadIdx.x < 64) {
+    const int64_t j = bj + threadIdx.x - 32;
+    beta[threadIdx.x - 32] = j < n ? pow(k_item[j], lambda) : 1.0;
+  }
+  if (transpose) {
+    for (int yy = ty; yy < 32; yy += 8) {
+      const int64_t si = bj + yy, sj = bi + tx;  // source row = output column
+      tile[yy][tx] = (si < n && sj < n) ? gW[si * n + sj] : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int64_t i = bi + yy, j = bj + tx;
+    if (i >= n || j >= n) continue;
+    const double src = transpose ? tile[tx][yy] : gW[i * n + j];
+    double den = alpha[yy] * beta[tx];
+    if (den == 0.0) den = 1.0;
+    W[i * n + j] = src / den;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_spread_resource(
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    const double *__restrict__ W, int64_t n_items, double *__restrict__ F, int64_t ldf) {
+  const int64_t u = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_items) return;
+  const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
+  double s = 0.0;
+  int64_t p = pb;
+  for (; p + 4 <= pe; p += 4) {
+    const double w0 = W[(int64_t)user_items[p] * n_items + j];
+    const double w1 = W[(int64_t)user_items[p + 1] * n_items + j];
+    const double w2 = W[(int64_t)user_items[p + 2] * n_items + j];
+    const double w3 = W[(int64_t)user_items[p + 3] * n_items + j];
+    s = (((s + w0) + w1) + w2) + w3;
+  }
+  for (; p < pe; ++p) s += W[(int64_t)user_items[p] * n_items + j];
+  F[u * ldf + j] = s;
+}
+
+// fp32 score in the chain order of lg_score_topk_f32 (see topk.hip header).
+template <int D>
+__device__ __forceinline__ float chain_score(const float *__restrict__ us,
+                                             const float *__restrict__ it) {
+  constexpr int Q = D / 4;
+  float r[D];
+  const float4 *p4 = reinterpret_cast<const float4 *>(it);
+#pragma unroll
+  for (int t = 0; t < D / 4; ++t) {
+    const float4 q = p4[t];
+    r[4 * t] = q.x;
+    r[4 * t + 1] = q.y;
+    r[4 * t + 2] = q.z;
+    r[4 * t + 3] = q.w;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int s = 0; s < Q; ++s)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc = __builtin_fmaf(us[g * Q + s], r[g * Q + s], acc);
+  return acc;
+}
+
+// One wave per row. D == 0: no G factor.
+template <int M, int D>
+__global__ __launch_bounds__(256) void k_rows_topk(
+    const double *__restrict__ F, int64_t ldf, int64_t n_rows, int64_t n_cols,
+    const float *__restrict__ eu, const float *__restrict__ ei,
+    const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col, int excl_mode,
+    int k, double *__restrict__ out_val, int64_t *__restrict__ out_idx) {
+  constexpr int CAP = 64 * M;
+  constexpr int DU = D > 0 ? D : 1;
+  __shared__ double cs[4][CAP];
+  __shared__ int ci[4][CAP];
+  __shared__ float us[4][DU];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= n_rows) return;
+  if (D > 0) {
+    for (int t = lane; t < D; t += 64) us[wave][t] = eu[r * D + t];
+    wave_sync();
+  }
+  int64_t lo = 0, hi = 0;
+  if (ex_rowptr && excl_mode == LG_EXCL_DROP) {
+    lo = ex_rowptr[r];
+    hi = ex_rowptr[r + 1];
+  }
+  int cnt = 0;
+  double tau = neg_inf<double>();
+  int tau_id = kPadId;
+  const double *row = F + r * ldf;
+  for (int64_t j0 = 0; j0 < n_cols; j0 += 64) {
+    const int64_t j = j0 + lane;
+    const bool valid = j < n_cols;
+    double v = valid ? row[j] : neg_inf<double>();
+    if (D > 0 && valid) v = (double)chain_score<DU>(us[wave], ei + j * D) * v;
+    // columns arrive in ascending order, so a tie with tau loses: plain '>' is exact
+    bool cand = valid && v > tau;
+    if (__ballot(cand)) {
+      if (cand && lo < hi) {
+        const int64_t p = lower_bound_i32(ex_col, lo, hi, (int32_t)j);
+        lo = p;
+        if (p < hi && ex_col[p] == (int32_t)j) cand = false;
+      }
+      const uint64_t bal = __ballot(cand);
+      const int pos = cnt + __popcll(bal & lanemask_lt());
+      if (cand) {
+        cs[wave][pos] = v;
+        ci[wave][pos] = (int)j;
+      }
+      cnt += __popcll(bal);
+      if (cnt > CAP - 64) {
+        wave_sync();
+        cnt = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+      }
+    }
+  }
+  wave_sync();
+  const int nc = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+  for (int e = lane; e < k; e += 64) {
+    out_val[r * k + e] = e < nc ? cs[wave][e] : neg_inf<double>();
+    out_idx[r * k + e] = e < nc ? ci[wave][e] : -1;
+  }
+}
+
+template <int M>
+static void launch_rows_topk(int dim, const double *F, int64_t ldf, int64_t n_rows,
+                             int64_t n_cols, const float *eu, const float *ei,
+                             const int64_t *ex_rowptr, const int32_t *ex_col, int excl_mode,
+                             int k, double *out_val, int64_t *out_idx, hipStream_t s) {
+  dim3 grid((unsigned)((n_rows + 3) / 4)), block(256);
+  switch (eu ? dim : 0) {
+    case 0: k_rows_topk<M, 0><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    case 32: k_rows_topk<M, 32><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    case 64: k_rows_topk<M, 64><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    default: k_rows_topk<M, 128><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+  }
+}
+
+}  // namespace lg
+
+using namespace lg;
+
+extern "C" int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                                     const int64_t *user_rowptr, const int32_t *user_items,
+                                     int64_t n_users, int64_t n_items, double *gW,
+                                     lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_rowptr && gW && n_users >= 0 && n_items >= 0,
+             "lg_spread_general_f64: bad arguments");
+  if (n_items == 0) return LG_OK;
+  k_spread_general<<<dim3((unsigned)n_items), dim3(256), 0, (hipStream_t)stream>>>(
+      item_rowptr, item_users, user_rowptr, user_items, n_items, gW);
+  return launch_status("lg_spread_general_f64");
+}
+
+extern "C" int lg_hybrid_weight_f64(const double *gW, const double *k_item, int64_t n_items,
+                                    double lambda, int32_t transpose_gw, double *W,
+                                    lg_stream_t stream) {
+  LG_REQUIRE(gW && k_item && W && n_items >= 0, "lg_hybrid_weight_f64: bad arguments");
+  LG_REQUIRE(gW != W || !transpose_gw, "lg_hybrid_weight_f64: transposed source cannot alias W");
+  if (n_items == 0) return LG_OK;
+  const unsigned t = (unsigned)((n_items + 31) / 32);
+  k_hybrid_weight<<<dim3(t, t), dim3(256), 0, (hipStream_t)stream>>>(gW, k_item, lambda, n_items,
+                                                                    transpose_gw, W);
+  return launch_status("lg_hybrid_weight_f64");
+}
+
+extern "C" int lg_spread_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
+                                      const double *W, int64_t n_users, int64_t n_items,
+                                      double *F, int64_t ldf, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && W && F && n_users >= 0 && n_items >= 0 && ldf >= n_items,
+             "lg_spread_resource_f64: bad arguments");
+  if (n_users == 0 || n_items == 0) return LG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  // grid.y is limited to 65535: walk users in slabs
+  for (int64_t u0 = 0; u0 < n_users; u0 += 65535) {
+    const int64_t nu = (n_users - u0) < 65535 ? (n_users - u0) : 65535;
+    k_spread_resource<<<dim3((unsigned)((n_items + 255) / 256), (unsigned)nu), dim3(256), 0,
+                        s>>>(user_rowptr + u0, user_items, W, n_items, F + u0 * ldf, ldf);
+  }
+  return launch_status("lg_spread_resource_f64");
+}
+
+extern "C" int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows,
+                                int64_t n_cols, const float *eu, const float *ei,
+                                int32_t dim, const int64_t *ex_rowptr,
+                                const int32_t *ex_col, int32_t excl_mode, int32_t k,
+                                double *out_val, int64_t *out_idx, lg_stream_t stream) {
+  LG_REQUIRE(F && out_val && out_idx && n_rows >= 0 && n_cols >= 0 && ldf >= n_cols &&
+                 n_cols < 0x7fffffff,
+             "lg_rows_topk_f64: bad arguments");
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_rows_topk_f64: k=%d not in [1,128]", k);
+  LG_REQUIRE(!eu == !ei, "lg_rows_topk_f64: eu/ei must both be set or both NULL");
+  LG_REQUIRE(!eu || dim == 32 || dim == 64 || dim == 128,
+             "lg_rows_topk_f64: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(excl_mode == LG_EXCL_DROP || excl_mode == LG_EXCL_NONE,
+             "lg_rows_topk_f64: bad excl_mode %d", excl_mode);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_rows_topk_f64: ex_rowptr/ex_col must both be set");
+  LG_REQUIRE(!(eu && excl_mode == LG_EXCL_NONE && ex_rowptr),
+             "lg_rows_topk_f64: a G factor with exclusions requires LG_EXCL_DROP");
+  if (n_rows == 0) return LG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (k <= 64)
+    launch_rows_topk<2>(dim, F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k,
+                        out_val, out_idx, s);
+  else
+    launch_rows_topk<4>(dim, F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k,
+                        out_val, out_idx, s);
+  return launch_status("lg_rows_topk_f64");
+}

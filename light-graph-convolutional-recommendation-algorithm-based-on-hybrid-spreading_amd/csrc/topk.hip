@@ -1,0 +1,418 @@
+// K2: full-catalog scoring + exclusion mask + streaming top-K, gfx950 f32 MFMA.
+//
+// Replaces model/LightGCN/recommend.py:83-114 (identical in LightGCNOpti/recommend.py and
+// LightGCN/evaluation.py:31-51):
+//     score = torch.matmul(users_emb.weight, items_emb.weight.T)       # [U, I] fp32
+//     score[train positives] = -(1 << 10); score[val positives] = -(1 << 10)
+//     _, recommendations = torch.topk(score, k)
+// and the dense masked matrix of getAllocateMat (model/SpreadLightGCN/model.py:74-104).
+//
+// Score definition (bit-exact, checked against oracle/score_chain.c): v_mfma_f32_16x16x4_f32
+// computes a k-ordered fp32 fma chain. Lane l of a wave holds item row (l & 15) as the A
+// operand and user column (l & 15) as the B operand, k-slot (l >> 4); step s of the chain
+// uses element g*Q + s of k-slot g (Q = D/4), so each lane reads one contiguous 16*Q-byte
+// piece of each embedding row, and the fp32 result equals
+//     acc = 0; for s < Q: for g < 4: acc = fmaf(u[g*Q+s], i[g*Q+s], acc).
+// Top-K: per user a candidate list of CAP entries in LDS; a score enters only if it beats
+// the user's current K-th best (tau), so after the first few hundred items almost nothing
+// enters and the VALU cost per score is one compare. The exclusion row (sorted) is
+// binary-searched only for entering candidates: an excluded item takes mask_value (-1024)
+// and is re-tested, which is exactly the reference's masked top-k. Lists are compacted by
+// the wave-wide bitonic sort of common.h. Order: (score desc, item asc).
+#include "common.h"
+
+namespace lg {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int Q>
+__device__ __forceinline__ void load_piece(const float *__restrict__ p, float (&v)[Q]) {
+  const float4 *p4 = reinterpret_cast<const float4 *>(p);
+#pragma unroll
+  for (int t = 0; t < Q / 4; ++t) {
+    const float4 q = p4[t];
+    v[4 * t + 0] = q.x;
+    v[4 * t + 1] = q.y;
+    v[4 * t + 2] = q.z;
+    v[4 * t + 3] = q.w;
+  }
+}
+
+// One wave: NG groups of 16 users; the block's waves work independently.
+template <int D, int NG, int M, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_score_topk(
+    const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
+    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
+  constexpr int Q = D / 4;
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[WAVES][NG][16][CAP];
+  __shared__ int ci[WAVES][NG][16][CAP];
+
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  const int64_t tile = blockIdx.x / n_splits;
+  const int split = blockIdx.x % n_splits;
+  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
+  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  const int64_t i0 = (int64_t)split * items_per_split;
+  int64_t i1 = i0 + items_per_split;
+  if (i1 > n_items) i1 = n_items;
+
+  float uf[NG][Q];
+  bool uvalid[NG];
+  int64_t ex_lo[NG], ex_hi[NG];
+  int cnt[NG];
+  float tau[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t u = ubase + g * 16 + ul;
+    uvalid[g] = u < n_users;
+    const int64_t uu = uvalid[g] ? u : n_users - 1;
+    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+    ex_lo[g] = 0;
+    ex_hi[g] = 0;
+    if (ex_rowptr && uvalid[g]) {
+      ex_lo[g] = ex_rowptr[u];
+      ex_hi[g] = ex_rowptr[u + 1];
+    }
+    cnt[g] = 0;
+    tau[g] = neg_inf<float>();
+  }
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+
+  for (int64_t it = i0; it < i1; it += 16) {
+    const int64_t item_l = it + ul;
+    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
+    float af[Q];
+    load_piece<Q>(ei + itc * D + gq * Q, af);
+
+    f32x4 acc[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < Q; ++s)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
+    }
+
+    // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t item = it + gq * 4 + r;
+        float sc = acc[g][r];
+        bool cand = uvalid[g] && item < i1 && sc > tau[g];
+        if (__ballot(cand)) {
+          if (cand && ex_lo[g] < ex_hi[g]) {
+            const int64_t p = lower_bound_i32(ex_col, ex_lo[g], ex_hi[g], (int32_t)item);
+            ex_lo[g] = p;  // this lane's later items are larger
+            if (p < ex_hi[g] && ex_col[p] == (int32_t)item) {
+              sc = mask_value;
+              cand = sc > tau[g];
+            }
+          }
+          const uint64_t bal = __ballot(cand);
+          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][pos] = sc;
+            ci[wave][g][ul][pos] = (int)item;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+
+    // compact every user whose list could overflow on the next tile (+16 max per tile)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+      if (need) {
+        wave_sync();
+        while (need) {
+          const int u = __ffsll((long long)need) - 1;
+          need &= need - 1;
+          const int n = __shfl(cnt[g], u);
+          float t;
+          int tid;
+          const int nc = wave_compact<float, M>(&cs[wave][g][u][0], &ci[wave][g][u][0], n, k,
+                                                t, tid);
+          if (ul == u) {
+            cnt[g] = nc;
+            tau[g] = t;
+          }
+        }
+      }
+    }
+  }
+
+  // final lists
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t user = ubase + g * 16 + u;
+      if (user >= n_users) break;
+      const int n = __shfl(cnt[g], u);
+      float t;
+      int tid;
+      const int nc =
+          wave_compact<float, M>(&cs[wave][g][u][0], &ci[wave][g][u][0], n, k, t, tid);
+      for (int e = lane; e < k; e += 64) {
+        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
+        const int id = e < nc ? ci[wave][g][u][e] : -1;
+        if (n_splits == 1) {
+          out_val[user * k + e] = v;
+          out_idx[user * k + e] = id;
+        } else {
+          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          part_val[o] = v;
+          part_idx[o] = id;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
+template <int M>
+__global__ __launch_bounds__(256) void k_topk_merge(const float *__restrict__ part_val,
+                                                    const int32_t *__restrict__ part_idx,
+                                                    int64_t n_users, int k, int n_splits,
+                                                    float *__restrict__ out_val,
+                                                    int64_t *__restrict__ out_idx) {
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[4][CAP];
+  __shared__ int ci[4][CAP];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int64_t user = (int64_t)blockIdx.x * 4 + wave;
+  if (user >= n_users) return;
+  int cnt = 0;
+  float tau = neg_inf<float>();
+  int tau_id = kPadId;
+  for (int s = 0; s < n_splits; ++s) {
+    const int64_t base = ((int64_t)s * n_users + user) * k;
+    for (int e0 = 0; e0 < k; e0 += 64) {
+      const int e = e0 + lane;
+      float v = neg_inf<float>();
+      int id = -1;
+      if (e < k) {
+        v = part_val[base + e];
+        id = part_idx[base + e];
+      }
+      const bool cand = id >= 0 && before(v, id, tau, tau_id);
+      const uint64_t bal = __ballot(cand);
+      const int pos = cnt + __popcll(bal & lanemask_lt());
+      if (cand) {
+        cs[wave][pos] = v;
+        ci[wave][pos] = id;
+      }
+      cnt += __popcll(bal);
+      if (cnt > CAP - 64) {
+        wave_sync();
+        cnt = wave_compact<float, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+      }
+    }
+  }
+  wave_sync();
+  const int nc = wave_compact<float, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+  for (int e = lane; e < k; e += 64) {
+    out_val[user * k + e] = e < nc ? cs[wave][e] : neg_inf<float>();
+    out_idx[user * k + e] = e < nc ? ci[wave][e] : -1;
+  }
+}
+
+// Dense masked score tile writer: G[u][i] for a 16-user x 16-item MFMA tile per step.
+template <int D>
+__global__ __launch_bounds__(256) void k_score_dense(
+    const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, float *__restrict__ G,
+    int64_t ldg, int64_t items_per_block) {
+  constexpr int Q = D / 4;
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  // blockIdx.x -> (user group of 64 users = 4 waves x 16, item chunk)
+  const int64_t n_chunks = (n_items + items_per_block - 1) / items_per_block;
+  const int64_t ugrp = blockIdx.x / n_chunks;
+  const int64_t chunk = blockIdx.x % n_chunks;
+  const int64_t u = ugrp * 64 + wave * 16 + ul;
+  const bool uvalid = u < n_users;
+  const int64_t uu = uvalid ? u : n_users - 1;
+  if (ugrp * 64 + wave * 16 >= n_users) return;
+  float uf[Q];
+  load_piece<Q>(eu + uu * D + gq * Q, uf);
+  const int64_t i0 = chunk * items_per_block;
+  int64_t i1 = i0 + items_per_block;
+  if (i1 > n_items) i1 = n_items;
+  // exclusion pointer: this lane's items (it + 4gq + r) increase across tiles
+  int64_t lo = 0, hi = 0;
+  if (ex_rowptr && uvalid) {
+    lo = ex_rowptr[u];
+    hi = ex_rowptr[u + 1];
+    lo = lower_bound_i32(ex_col, lo, hi, (int32_t)i0);
+  }
+  for (int64_t it = i0; it < i1; it += 16) {
+    const int64_t item_l = it + ul;
+    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
+    float af[Q];
+    load_piece<Q>(ei + itc * D + gq * Q, af);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < Q; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[s], acc, 0, 0, 0);
+    if (uvalid) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t item = it + gq * 4 + r;
+      v[r] = acc[r];
+      while (lo < hi && ex_col[lo] < (int32_t)item) ++lo;
+      if (lo < hi && ex_col[lo] == (int32_t)item) v[r] = mask_value;
+    }
+    const int64_t c0 = it + gq * 4;
+    float *row = G + u * ldg;
+    if (c0 + 3 < i1 && ((ldg & 3) == 0)) {
+      *reinterpret_cast<float4 *>(row + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (c0 + r < i1) row[c0 + r] = v[r];
+    }
+    }
+  }
+}
+
+template <int D, int NG, int M, int WAVES>
+static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
+                        const int64_t *ex_rowptr, const int32_t *ex_col, float mask_value,
+                        int k, int n_splits, int64_t items_per_split, float *out_val,
+                        int64_t *out_idx, float *part_val, int32_t *part_idx,
+                        hipStream_t stream) {
+  const int64_t users_per_block = (int64_t)WAVES * NG * 16;
+  const int64_t tiles = (n_users + users_per_block - 1) / users_per_block;
+  k_score_topk<D, NG, M, WAVES><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
+                                   stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
+                                             mask_value, k, n_splits, items_per_split,
+                                             out_val, out_idx, part_val, part_idx);
+}
+
+template <int D>
+static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_users,
+                          int64_t n_items, const int64_t *ex_rowptr, const int32_t *ex_col,
+                          float mask_value, int k, int n_splits, int64_t items_per_split,
+                          float *out_val, int64_t *out_idx, float *part_val,
+                          int32_t *part_idx, hipStream_t stream) {
+  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB in every configuration.
+  if (M == 1)
+    launch_topk<D, 2, 1, 4>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else if (M == 2)
+    launch_topk<D, 2, 2, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else
+    launch_topk<D, 1, 4, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+}
+
+static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
+
+static int64_t split_len(int64_t n_items, int n_splits) {
+  int64_t per = (n_items + n_splits - 1) / n_splits;
+  per = (per + 15) / 16 * 16;
+  return per < 16 ? 16 : per;
+}
+
+}  // namespace lg
+
+using namespace lg;
+
+extern "C" size_t lg_score_topk_ws_bytes(int64_t n_users, int64_t n_items, int32_t dim,
+                                         int32_t k, int32_t n_splits) {
+  (void)n_items;
+  (void)dim;
+  if (n_splits <= 1 || n_users <= 0 || k <= 0) return 0;
+  return (size_t)n_splits * (size_t)n_users * (size_t)k * (sizeof(float) + sizeof(int32_t));
+}
+
+extern "C" int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users,
+                                 int64_t n_items, int32_t dim, const int64_t *ex_rowptr,
+                                 const int32_t *ex_col, float mask_value, int32_t k,
+                                 int32_t n_splits, float *out_val, int64_t *out_idx,
+                                 void *ws, size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && out_val && out_idx, "lg_score_topk_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items > 0 && n_items < 0x7fffffff,
+             "lg_score_topk_f32: n_items must be in [1, 2^31-1)");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_topk_f32: dim %d not in {32,64,128}",
+             dim);
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_score_topk_f32: k=%d not in [1,128]", k);
+  LG_REQUIRE(n_splits >= 1 && n_splits <= 4096, "lg_score_topk_f32: bad n_splits %d", n_splits);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_score_topk_f32: ex_rowptr/ex_col must both be set");
+  if (n_users == 0) return LG_OK;
+  const int64_t per = split_len(n_items, n_splits);
+  const int ns = (int)((n_items + per - 1) / per);
+  float *part_val = nullptr;
+  int32_t *part_idx = nullptr;
+  if (ns > 1) {
+    const size_t need = lg_score_topk_ws_bytes(n_users, n_items, dim, k, ns);
+    if (!ws || ws_bytes < need) {
+      set_error("lg_score_topk_f32: workspace %zu < %zu bytes", ws_bytes, need);
+      return LG_ERR_WORKSPACE;
+    }
+    part_val = (float *)ws;
+    part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int M = cap_m(k);
+  switch (dim) {
+    case 32: dispatch_topk<32>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    case 64: dispatch_topk<64>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    default: dispatch_topk<128>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+  }
+  int st = launch_status("lg_score_topk_f32");
+  if (st != LG_OK || ns == 1) return st;
+  const unsigned blocks = (unsigned)((n_users + 3) / 4);
+  if (k <= 64)
+    k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  else
+    k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  return launch_status("lg_score_topk_f32(merge)");
+}
+
+extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_users,
+                                  int64_t n_items, int32_t dim, const int64_t *ex_rowptr,
+                                  const int32_t *ex_col, float mask_value, float *G,
+                                  int64_t ldg, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && G, "lg_score_dense_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items >= 0 && n_items < 0x7fffffff && ldg >= n_items,
+             "lg_score_dense_f32: bad sizes");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_dense_f32: dim %d not in {32,64,128}",
+             dim);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_score_dense_f32: ex_rowptr/ex_col must both be set");
+  if (n_users == 0 || n_items == 0) return LG_OK;
+  const int64_t ipb = 1024;
+  const int64_t chunks = (n_items + ipb - 1) / ipb;
+  const int64_t ugrps = (n_users + 63) / 64;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)(ugrps * chunks)), block(256);
+  switch (dim) {
+    case 32: k_score_dense<32><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+    case 64: k_score_dense<64><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+    default: k_score_dense<128><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+  }
+  return launch_status("lg_score_dense_f32");
+}

@@ -1,0 +1,237 @@
+"""Torch-facing wrappers of the HIP hot path (no CPU fallback: GPU tensors only).
+
+propagate        LightGCN layers + layer mean      model/LightGCN/model.py:53-74
+score_topk       e0 scores, -1024 mask, top-k      model/LightGCN/recommend.py:83-114
+score_dense      masked dense score matrix G       model/SpreadLightGCN/model.py:74-104
+spread_general   general_W                         model/SpreadMethod/model.py:14-27
+hybrid_weight    HybridS W                         model/SpreadMethod/model.py:63-85
+spread_resource  F = A @ W                         model/SpreadMethod/model.py:88-99
+rows_topk        argsort + filter + [:k], G * F    model/SpreadMethod/recommend.py:31-50,
+                                                   model/SpreadLightGCN/model.py:151
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+from .graph import Adjacency, RowSets
+
+MASK_VALUE = float(-(1 << 10))  # model/LightGCN/recommend.py:101,111
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    N.require_gpu(t, name)
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------------------ propagation
+def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
+               row_begin: int = 0, row_end: int | None = None, dis=None,
+               rowptr=None, src=None) -> None:
+    """One lg_spmm_layer_f32 launch over rows [row_begin, row_end) of ``adj``."""
+    if row_end is None:
+        row_end = adj.n_nodes
+    rp = adj.rowptr if rowptr is None else rowptr
+    sr = adj.src if src is None else src
+    ds = adj.dis() if dis is None else dis
+    N.check(N.lib().lg_spmm_layer_f32(
+        N.ptr(rp[row_begin:] if rowptr is None else rp), N.ptr(sr), N.ptr(ds), N.ptr(x),
+        N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), row_end - row_begin, row_begin,
+        x.shape[1], mode, float(denom), N.stream_handle(x.device)), "lg_spmm_layer_f32")
+
+
+def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:
+    """mean_{l=0..L} A_hat^l e0 with A_hat = D^-1/2 A D^-1/2 (no autograd)."""
+    e0 = _f32(e0, "e0")
+    if e0.shape[0] != adj.n_nodes:
+        raise ValueError(f"e0 has {e0.shape[0]} rows, graph has {adj.n_nodes} nodes")
+    if layers <= 0:
+        return e0.clone()
+    out = torch.empty_like(e0)
+    bufs = [torch.empty_like(e0), torch.empty_like(e0) if layers > 2 else None]
+    x = e0
+    for l in range(layers):
+        first, last = l == 0, l == layers - 1
+        if first and last:
+            mode = N.LG_ACC_ONLY
+        elif first:
+            mode = N.LG_ACC_FIRST
+        elif last:
+            mode = N.LG_ACC_LAST
+        else:
+            mode = N.LG_ACC_MID
+        y = None if last else bufs[l % 2]
+        spmm_layer(adj, x, y, e0, out, out, mode, layers + 1)
+        x = y
+    return out
+
+
+class _Propagate(torch.autograd.Function):
+    """Forward: mean of the L+1 layer embeddings. Backward: the same operator with A_hat^T
+    (A_hat itself for the symmetric LightGCN graph): grad_e0 = mean_l (A_hat^T)^l g."""
+
+    @staticmethod
+    def forward(ctx, e0, adj, layers):
+        ctx.adj, ctx.layers = adj, layers
+        return propagate_mean(adj, e0.detach(), layers)
+
+    @staticmethod
+    def backward(ctx, g):
+        gin = propagate_mean(ctx.adj.transpose(), g.contiguous(), ctx.layers)
+        return gin, None, None
+
+
+def propagate(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:
+    if e0.requires_grad and torch.is_grad_enabled():
+        return _Propagate.apply(e0, adj, layers)
+    return propagate_mean(adj, e0, layers)
+
+
+# ------------------------------------------------------------------------------ scoring
+def _splits_for(n_users: int, n_items: int, k: int) -> int:
+    per_block = 128 if k <= 32 else (64 if k <= 64 else 32)
+    tiles = (n_users + per_block - 1) // per_block
+    target_blocks = 2048
+    if tiles >= target_blocks:
+        return 1
+    want = (target_blocks + tiles - 1) // tiles
+    return max(1, min(want, (n_items + 255) // 256))
+
+
+def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None = None,
+               mask_value: float = MASK_VALUE, n_splits: int | None = None):
+    """Top-k items per user by the masked e0 score; returns (values fp32 [U,k],
+    indices int64 [U,k]) sorted by (score desc, item asc)."""
+    eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
+    nu, d = eu.shape
+    ni = ei.shape[0]
+    if ei.shape[1] != d:
+        raise ValueError("eu/ei dims differ")
+    if excl is not None and excl.n_rows != nu:
+        raise ValueError(f"exclusion rows {excl.n_rows} != users {nu}")
+    ns = _splits_for(nu, ni, k) if n_splits is None else int(n_splits)
+    ws_bytes = N.lib().lg_score_topk_ws_bytes(nu, ni, d, k, ns)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
+    val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)
+    idx = torch.empty((nu, k), dtype=torch.int64, device=eu.device)
+    N.check(N.lib().lg_score_topk_f32(
+        N.ptr(eu), N.ptr(ei), nu, ni, d, N.ptr(excl.rowptr if excl else None),
+        N.ptr(excl.col if excl else None), float(mask_value), int(k), ns, N.ptr(val),
+        N.ptr(idx), N.ptr(ws), ws_bytes, N.stream_handle(eu.device)), "lg_score_topk_f32")
+    return val, idx
+
+
+def score_dense(eu: torch.Tensor, ei: torch.Tensor, excl: RowSets | None = None,
+                mask_value: float = MASK_VALUE) -> torch.Tensor:
+    eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
+    nu, d = eu.shape
+    ni = ei.shape[0]
+    G = torch.empty((nu, ni), dtype=torch.float32, device=eu.device)
+    N.check(N.lib().lg_score_dense_f32(
+        N.ptr(eu), N.ptr(ei), nu, ni, d, N.ptr(excl.rowptr if excl else None),
+        N.ptr(excl.col if excl else None), float(mask_value), N.ptr(G), ni,
+        N.stream_handle(eu.device)), "lg_score_dense_f32")
+    return G
+
+
+# ------------------------------------------------------------------------------ spreading
+class Interactions:
+    """The 0/1 interaction matrix A held sparse both ways, with degrees as fp64."""
+
+    def __init__(self, by_user: RowSets):
+        self.by_user = by_user
+        self.by_item = by_user.transpose()
+        self.n_users, self.n_items = by_user.n_rows, by_user.n_cols
+        self.k_user = by_user.degrees().to(torch.float64)
+        self.k_item = self.by_item.degrees().to(torch.float64)
+
+    @classmethod
+    def from_pairs(cls, users, items, n_users, n_items, device=None):
+        return cls(RowSets.from_pairs(users, items, n_users, n_items, device))
+
+    @classmethod
+    def from_dense(cls, A: torch.Tensor):
+        """From a dense [U, I] matrix (nonzero = interaction), e.g. the reference's A."""
+        N.require_gpu(A, "A")
+        nz = torch.nonzero(A != 0)
+        return cls.from_pairs(nz[:, 0], nz[:, 1], A.shape[0], A.shape[1], A.device)
+
+
+def spread_general(A: Interactions) -> torch.Tensor:
+    gW = torch.empty((A.n_items, A.n_items), dtype=torch.float64, device=A.k_item.device)
+    N.check(N.lib().lg_spread_general_f64(
+        N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.rowptr),
+        N.ptr(A.by_user.col), A.n_users, A.n_items, N.ptr(gW),
+        N.stream_handle(gW.device)), "lg_spread_general_f64")
+    return gW
+
+
+def hybrid_weight(gW: torch.Tensor, k_item: torch.Tensor, lam: float,
+                  transpose: bool = False) -> torch.Tensor:
+    N.require_gpu(gW, "gW")
+    gW = gW.contiguous().to(torch.float64)
+    k_item = k_item.contiguous().to(torch.float64)
+    W = torch.empty_like(gW)
+    N.check(N.lib().lg_hybrid_weight_f64(N.ptr(gW), N.ptr(k_item), gW.shape[0], float(lam),
+                                         int(bool(transpose)), N.ptr(W),
+                                         N.stream_handle(gW.device)), "lg_hybrid_weight_f64")
+    return W
+
+
+def spread_resource(A: Interactions, W: torch.Tensor, users: slice | None = None,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """F rows for users [u0, u1) (all by default)."""
+    u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
+    W = W.contiguous()
+    F = out if out is not None else torch.empty((u1 - u0, A.n_items), dtype=torch.float64,
+                                                device=W.device)
+    N.check(N.lib().lg_spread_resource_f64(
+        N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), N.ptr(W), u1 - u0, A.n_items,
+        N.ptr(F), F.stride(0), N.stream_handle(W.device)), "lg_spread_resource_f64")
+    return F
+
+
+def rows_topk(F: torch.Tensor, k: int, excl: RowSets | None = None, drop: bool = True,
+              eu: torch.Tensor | None = None, ei: torch.Tensor | None = None):
+    """Per-row top-k of F (optionally times the fp32 score G = eu . ei), excluded columns
+    dropped (drop=True) or kept (drop=False). Returns (values fp64, indices int64, -1 pad)."""
+    N.require_gpu(F, "F")
+    if F.dtype != torch.float64:
+        raise TypeError("F must be float64")
+    if F.stride(1) != 1:
+        F = F.contiguous()
+    n, m = F.shape
+    d = 0
+    if eu is not None:
+        eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
+        d = eu.shape[1]
+    val = torch.empty((n, k), dtype=torch.float64, device=F.device)
+    idx = torch.empty((n, k), dtype=torch.int64, device=F.device)
+    N.check(N.lib().lg_rows_topk_f64(
+        N.ptr(F), F.stride(0), n, m, N.ptr(eu), N.ptr(ei), d,
+        N.ptr(excl.rowptr if excl else None), N.ptr(excl.col if excl else None),
+        N.LG_EXCL_DROP if drop else N.LG_EXCL_NONE, int(k), N.ptr(val), N.ptr(idx),
+        N.stream_handle(F.device)), "lg_rows_topk_f64")
+    return val, idx
+
+
+def spread_topk(A: Interactions, W: torch.Tensor, k: int, excl: RowSets | None,
+                drop: bool = True, eu: torch.Tensor | None = None,
+                ei: torch.Tensor | None = None, block_users: int | None = None):
+    """F = A @ W computed block by block and reduced to per-user top-k without ever
+    holding all of F (the fused recommend path of SpreadMethod / SpreadLightGCN)."""
+    U, I = A.n_users, A.n_items
+    if block_users is None:
+        block_users = max(1, min(U, (1 << 30) // max(1, I * 8)))  # ~1 GiB of F per block
+    vals = torch.empty((U, k), dtype=torch.float64, device=W.device)
+    idxs = torch.empty((U, k), dtype=torch.int64, device=W.device)
+    buf = torch.empty((min(block_users, U), I), dtype=torch.float64, device=W.device)
+    for u0 in range(0, U, block_users):
+        u1 = min(U, u0 + block_users)
+        Fb = spread_resource(A, W, slice(u0, u1), out=buf[: u1 - u0])
+        ex = excl.slice_rows(u0, u1) if excl is not None else None
+        v, i = rows_topk(Fb, k, ex, drop, None if eu is None else eu[u0:u1], ei)
+        vals[u0:u1], idxs[u0:u1] = v, i
+    return vals, idxs

@@ -1,0 +1,292 @@
+"""ORACLE — CPU restatement of the reference's hot path. TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the CPU baseline; the product package never
+imports it (tests/test_no_oracle_in_product.py enforces that).
+
+What it restates (reference = Alex-McAvoy/Light-Graph-Convolutional-Recommendation-
+Algorithm-based-on-Hybrid-Spreading @ 2025-12-05; citations are file:line there):
+
+* utils/graph.py:12-35     convertEdgeIndexToAdjMatrix -> coalesced symmetric COO
+* PyG 2.6.1 (torch-geometric==2.6.1, environment.yaml:276; absent from this image, so its
+  published algorithm is restated): gcn_norm(add_self_loops=False) and
+  MessagePassing.propagate(aggr='add', flow='source_to_target') as called by
+  model/LightGCN/model.py:53,62,84
+* model/LightGCN/model.py:32-38,40-74  init + forward (stack/mean/split)
+* model/LightGCN/recommend.py:83-114   e0 scoring, -1024 masks, torch.topk
+* model/SpreadLightGCN/model.py:74-104,151  getAllocateMat, G * F
+* model/SpreadMethod/model.py:14-99    getSpreadingGeneralMat, ProbS, HeatS, HybridS,
+                                        getResource
+* model/SpreadMethod/recommend.py:18-111 recommendForAllUser (argsort + filter, the
+                                        ML-ProbS unfiltered quirk), recommendSpreadMethod
+                                        (lambda / transpose overrides)
+* utils/trans.py:13-29,51-80           interaction matrix and user->items dicts
+
+Pinning: tests/golden/make_golden.py runs the reference's own importable modules
+(SpreadMethod, utils/trans) unmodified, and its LightGCN modules on top of a PyG 2.6.1
+restatement, to produce tests/golden/*.npz; tests/test_oracle_golden.py checks this
+oracle against those fixtures.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MASK = float(-(1 << 10))  # model/LightGCN/recommend.py:101,111
+
+
+# ----------------------------------------------------------------------------------
+# graph format: utils/graph.py:12-35
+# ----------------------------------------------------------------------------------
+def coo_adjacency(n_users: int, n_items: int, users, items) -> np.ndarray:
+    """convertEdgeIndexToAdjMatrix: R[u][i] = 1 (duplicates collapse), the symmetric
+    (U+I)^2 block matrix, ``to_sparse_coo().indices()``: int64 [2, nnz] sorted by
+    (row, col) with items offset by U."""
+    users = np.asarray(users, dtype=np.int64)
+    items = np.asarray(items, dtype=np.int64) + n_users
+    n = n_users + n_items
+    rows = np.concatenate([users, items])
+    cols = np.concatenate([items, users])
+    keys = np.unique(rows * n + cols)
+    return np.stack([keys // n, keys % n])
+
+
+def coo_to_interactions(n_users: int, n_items: int, edge_index: np.ndarray) -> np.ndarray:
+    """convertAdjMatrixToEdgeIndex (utils/graph.py:38-50): the user->item block of the
+    symmetric COO back as a sorted [2, E] (user, item) array."""
+    r, c = np.asarray(edge_index[0]), np.asarray(edge_index[1])
+    m = (r < n_users) & (c >= n_users)
+    keys = np.unique(r[m] * n_items + (c[m] - n_users))
+    return np.stack([keys // n_items, keys % n_items])
+
+
+# ----------------------------------------------------------------------------------
+# PyG 2.6.1 restated (torch CPU, fp32)
+# ----------------------------------------------------------------------------------
+def gcn_norm(edge_index: torch.Tensor, num_nodes: int | None = None):
+    """torch_geometric.nn.conv.gcn_conv.gcn_norm(edge_index, add_self_loops=False),
+    flow='source_to_target': deg = scatter_add(ones, col); dis = deg.pow(-0.5);
+    dis[inf] = 0; w = dis[row] * 1 * dis[col]."""
+    if num_nodes is None:
+        num_nodes = int(edge_index.max()) + 1 if edge_index.numel() else 0
+    row, col = edge_index[0], edge_index[1]
+    w = torch.ones(row.numel(), dtype=torch.float32)
+    deg = torch.zeros(num_nodes, dtype=torch.float32).scatter_add_(0, col, w)
+    dis = deg.pow(-0.5)
+    dis.masked_fill_(dis == float("inf"), 0)
+    return edge_index, dis[row] * w * dis[col]
+
+
+def propagate(edge_index: torch.Tensor, w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """MessagePassing.propagate, aggr='add': x_j = x.index_select(0, row);
+    msg = w.view(-1,1) * x_j (model/LightGCN/model.py:84); out[col] += msg."""
+    row, col = edge_index[0], edge_index[1]
+    msg = w.view(-1, 1) * x.index_select(0, row)
+    out = torch.zeros_like(x)
+    out.index_add_(0, col, msg)
+    return out
+
+
+def lightgcn_init(n_users: int, n_items: int, dim: int, seed: int = 42):
+    """model/LightGCN/model.py:32-38 under torch.manual_seed(seed)
+    (model/LightGCN/train.py:91): Embedding(U) then Embedding(I) are constructed (each
+    consuming its default N(0,1) init), then normal_(std=0.1) users, then items."""
+    torch.manual_seed(seed)
+    eu = torch.nn.Embedding(n_users, dim)
+    ei = torch.nn.Embedding(n_items, dim)
+    torch.nn.init.normal_(eu.weight, std=0.1)
+    torch.nn.init.normal_(ei.weight, std=0.1)
+    return eu.weight.detach().clone(), ei.weight.detach().clone()
+
+
+def lightgcn_forward(edge_index: torch.Tensor, emb_u: torch.Tensor, emb_i: torch.Tensor,
+                     layers: int):
+    """model/LightGCN/model.py:53-74: (users_final, items_final)."""
+    n_users = emb_u.shape[0]
+    n = n_users + emb_i.shape[0]
+    ei_norm, w = gcn_norm(edge_index, None)
+    emb = torch.cat([emb_u, emb_i])
+    embs = [emb]
+    for _ in range(layers):
+        emb = propagate(ei_norm, w, emb)
+        embs.append(emb)
+    final = torch.stack(embs, dim=1).mean(dim=1)
+    del n
+    return torch.split(final, [n_users, emb_i.shape[0]])
+
+
+# ----------------------------------------------------------------------------------
+# e0 scoring + masks + topk: model/LightGCN/recommend.py:83-114
+# ----------------------------------------------------------------------------------
+def masked_scores_torch(eu: torch.Tensor, ei: torch.Tensor, train_pairs, val_pairs):
+    """torch.matmul + the two -1024 index-puts (fp32, the reference's BLAS rounding)."""
+    score = torch.matmul(eu, ei.T)
+    for pairs in (train_pairs, val_pairs):
+        if pairs is not None and len(pairs[0]):
+            score[torch.as_tensor(pairs[0]), torch.as_tensor(pairs[1])] = MASK
+    return score
+
+
+def recommend_topk_torch(eu, ei, train_pairs, val_pairs, k: int):
+    score = masked_scores_torch(eu, ei, train_pairs, val_pairs)
+    vals, idx = torch.topk(score, k=k)
+    return vals, idx, score
+
+
+def exclusion_csr(n_users: int, n_items: int, *pair_sets):
+    """Sorted, de-duplicated union of (user, item) pair sets as (rowptr int64, col int32)."""
+    keys = [np.asarray(p[0], np.int64) * n_items + np.asarray(p[1], np.int64)
+            for p in pair_sets if p is not None]
+    keys = np.unique(np.concatenate(keys)) if keys else np.zeros(0, np.int64)
+    u = keys // n_items
+    rowptr = np.searchsorted(u, np.arange(n_users + 1), side="left").astype(np.int64)
+    return rowptr, (keys % n_items).astype(np.int32)
+
+
+# ----------------------------------------------------------------------------------
+# exact fp32 chain scores (C): oracle/score_chain.c
+# ----------------------------------------------------------------------------------
+_C = None
+
+
+def _clib():
+    global _C
+    if _C is None:
+        path = os.path.join(HERE, "build", "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+        lib = ctypes.CDLL(path)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.oracle_score_matrix.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp]
+        lib.oracle_score_topk.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp, vp,
+                                          ctypes.c_float, ctypes.c_int, vp, vp]
+        lib.oracle_score_topk.restype = ctypes.c_int
+        _C = lib
+    return _C
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else ctypes.c_void_p(0)
+
+
+def chain_scores(eu: np.ndarray, ei: np.ndarray) -> np.ndarray:
+    eu = np.ascontiguousarray(eu, np.float32)
+    ei = np.ascontiguousarray(ei, np.float32)
+    out = np.empty((eu.shape[0], ei.shape[0]), np.float32)
+    _clib().oracle_score_matrix(_p(eu), _p(ei), eu.shape[0], ei.shape[0], eu.shape[1],
+                                _p(out))
+    return out
+
+
+def chain_topk(eu, ei, ex_rowptr, ex_col, k: int, mask_value: float = MASK):
+    eu = np.ascontiguousarray(eu, np.float32)
+    ei = np.ascontiguousarray(ei, np.float32)
+    nu = eu.shape[0]
+    ov = np.empty((nu, k), np.float32)
+    oi = np.empty((nu, k), np.int64)
+    rp = None if ex_rowptr is None else np.ascontiguousarray(ex_rowptr, np.int64)
+    cl = None if ex_col is None else np.ascontiguousarray(ex_col, np.int32)
+    st = _clib().oracle_score_topk(_p(eu), _p(ei), nu, ei.shape[0], eu.shape[1], _p(rp),
+                                   _p(cl), mask_value, k, _p(ov), _p(oi))
+    assert st == 0
+    return ov, oi
+
+
+def chain_masked_matrix(eu, ei, ex_rowptr, ex_col, mask_value: float = MASK):
+    g = chain_scores(eu, ei)
+    for u in range(g.shape[0]):
+        g[u, ex_col[ex_rowptr[u]:ex_rowptr[u + 1]]] = mask_value
+    return g
+
+
+# ----------------------------------------------------------------------------------
+# hybrid spreading: model/SpreadMethod/model.py, utils/trans.py
+# ----------------------------------------------------------------------------------
+def interaction_matrix(n_users: int, n_items: int, users, items) -> np.ndarray:
+    """getInteractionMatrixByDataframe (utils/trans.py:13-29): dense fp64 A, A[u,i] = 1."""
+    A = np.zeros((n_users, n_items))
+    A[np.asarray(users, np.int64), np.asarray(items, np.int64)] = 1
+    return A
+
+
+def spreading_general_mat(A: np.ndarray) -> np.ndarray:
+    """getSpreadingGeneralMat (model/SpreadMethod/model.py:14-27)."""
+    ud = np.sum(A, axis=1)
+    ud[ud == 0] = 1
+    return np.dot(A.T / ud, A)
+
+
+def prob_s(A, gW):
+    """ProbS (model/SpreadMethod/model.py:30-43; never called by the reference)."""
+    kd = np.sum(A, axis=0)
+    kd[kd == 0] = 1
+    return gW / kd[np.newaxis, :]
+
+
+def heat_s(A, gW):
+    """HeatS (model/SpreadMethod/model.py:46-60; never called by the reference)."""
+    kd = np.sum(A, axis=0)
+    kd[kd == 0] = 1
+    return gW / kd[:, np.newaxis]
+
+
+def hybrid_s(A: np.ndarray, gW: np.ndarray, lam: float) -> np.ndarray:
+    """HybridS (model/SpreadMethod/model.py:63-85)."""
+    kd = np.sum(A, axis=0)
+    den = np.power(kd, 1 - lam)[:, np.newaxis] * np.power(kd, lam)[np.newaxis, :]
+    den[den == 0] = 1
+    return gW / den
+
+
+def get_resource(A, W):
+    """getResource (model/SpreadMethod/model.py:88-99)."""
+    return np.dot(A, W)
+
+
+def spread_overrides(method: str, dataset: str, lam: float, gW: np.ndarray):
+    """model/SpreadMethod/recommend.py:86-111: the lambda / transpose per method."""
+    if method == "ProbS" and dataset == "movielens":
+        return 0.01, gW.T
+    if method == "HeatS" and dataset == "douban":
+        return 0.99, gW.T
+    return lam, gW
+
+
+def recommend_all_user(F_new: np.ndarray, n_users: int, excl: dict, k: int,
+                       unfiltered: bool = False) -> dict:
+    """recommendForAllUser (model/SpreadMethod/recommend.py:18-56) with the canonical tie
+    order (value desc, item asc) in place of np.argsort's unspecified one."""
+    out = {}
+    for u in range(n_users):
+        row = F_new[u]
+        order = np.lexsort((np.arange(row.size), -row))
+        if unfiltered:
+            out[u] = order[:k].tolist()
+            continue
+        ex = set(excl.get(u, ()))
+        out[u] = [int(i) for i in order if int(i) not in ex][:k]
+    return out
+
+
+def rows_topk(F: np.ndarray, k: int, ex_rowptr=None, ex_col=None, drop: bool = True):
+    """Canonical (value desc, column asc) top-k per row with excluded columns dropped:
+    what lg_rows_topk_f64 must return bit for bit on the same F."""
+    n, m = F.shape
+    ov = np.full((n, k), -np.inf)
+    oi = np.full((n, k), -1, np.int64)
+    for r in range(n):
+        cols = np.arange(m)
+        vals = F[r]
+        if drop and ex_rowptr is not None:
+            keep = np.ones(m, bool)
+            keep[ex_col[ex_rowptr[r]:ex_rowptr[r + 1]]] = False
+            cols, vals = cols[keep], vals[keep]
+        order = np.lexsort((cols, -vals))[:k]
+        ov[r, :order.size] = vals[order]
+        oi[r, :order.size] = cols[order]
+    return ov, oi

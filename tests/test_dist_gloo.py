@@ -1,0 +1,92 @@
+"""World-size-2 (and 3) CPU run of the row-sharded propagation bookkeeping with the gloo
+backend: shard ranges, padding, per-layer all-gather and the fused layer-mean modes. The
+per-shard layer is the oracle's restatement (HIP kernels need a GPU), so this checks
+lgcnhs.dist exactly as bench.py drives it on RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import lgcn_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def cpu_layer(shard, dis, x, y, x0, acc, out, mode, denom):
+    """Oracle stand-in for lg_spmm_layer_f32 over the shard's rows."""
+    rp = shard.rowptr.numpy()
+    src = shard.src.numpy().astype(np.int64)
+    for r in range(shard.n_rows):
+        g = shard.r0 + r
+        s = src[rp[r]:rp[r + 1]]
+        w = dis[s] * dis[g]
+        v = (w[:, None] * x[s]).sum(0) if s.size else torch.zeros(x.shape[1])
+        if y is not None:
+            y[g] = v
+        if mode == 1:
+            acc[g] = x0[g] + v
+        elif mode == 2:
+            acc[g] = acc[g] + v
+        elif mode == 3:
+            out[g] = (acc[g] + v) / denom
+        elif mode == 4:
+            out[g] = (x0[g] + v) / denom
+
+
+def _worker(rank, world, port, U, I, users, items, layers, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lgcnhs.dist import RowShard, ShardedPropagation
+        n = U + I
+        coo = O.coo_adjacency(U, I, users, items)
+        # target-major CSR (symmetric graph: same as row-major)
+        rowptr = torch.as_tensor(np.searchsorted(coo[0], np.arange(n + 1)))
+        src = torch.as_tensor(coo[1].astype(np.int32))
+        deg = (rowptr[1:] - rowptr[:-1]).float()
+        dis = deg.pow(-0.5)
+        dis.masked_fill_(dis == float("inf"), 0)
+        shard = RowShard(rowptr, src, n, rank, world, "cpu")
+        torch.manual_seed(0)
+        e0 = torch.zeros(shard.n_pad, 8)
+        e0[:n] = torch.randn(n, 8) * 0.1
+        prop = ShardedPropagation(shard, dis, 8, layers, "cpu", layer_fn=cpu_layer)
+        out = prop.forward(e0, gather_out=True)
+        if rank == 0:
+            q.put(out[:n].numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,layers", [(2, 3), (2, 1), (3, 2)])
+def test_sharded_propagation_gloo(world, layers):
+    U, I = 13, 17
+    users, items = O.coo_to_interactions(U, I, O.coo_adjacency(U, I, *np.random.default_rng(1).integers(0, [U, I], (60, 2)).T))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, U, I, users, items, layers, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    n = U + I
+    e0 = torch.randn(n, 8) * 0.1
+    coo = torch.as_tensor(O.coo_adjacency(U, I, users, items))
+    uf, itf = O.lightgcn_forward(coo, e0[:U], e0[U:], layers)
+    np.testing.assert_allclose(got, torch.cat([uf, itf]).numpy(), atol=1e-6, rtol=0)

@@ -1,0 +1,128 @@
+"""GPU parity of the hybrid-spreading path (K3 general_W / HybridS / F, K4 row top-k with
+the G factor) against the reference's own numpy results (golden fixtures) and the oracle.
+fp64 tolerance: 1e-12 relative (only the summation order differs)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import lgcn_oracle as O
+from _compare import compare_topk_sets
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-12
+
+
+def _A(g):
+    U, I = int(g["n_users"]), int(g["n_items"])
+    both = np.concatenate([g["train"], g["val"]], axis=1).astype(np.int64)
+    return U, I, O.interaction_matrix(U, I, both[0], both[1])
+
+
+@pytest.mark.parametrize("name", ["spread_toy", "spread_edge"])
+def test_numpy_api_matches_reference(golden, name):
+    from model.SpreadMethod import model as sm
+    g = golden(name)
+    U, I, A = _A(g)
+    gW = sm.getSpreadingGeneralMat(A)
+    np.testing.assert_allclose(gW, g["gW"], rtol=RTOL, atol=0)
+    assert np.array_equal(gW, gW.T)  # ascending-order sums: exactly symmetric
+    for j, lam in enumerate(g["lambdas"]):
+        W = sm.HybridS(A, g["gW"], float(lam))
+        np.testing.assert_allclose(W, g[f"W_{j}"], rtol=RTOL, atol=0)
+        F = sm.getResource(A, W)
+        np.testing.assert_allclose(F, g[f"F_{j}"], rtol=RTOL, atol=1e-300)
+    if "probs_W" in g:
+        np.testing.assert_allclose(sm.ProbS(A, g["gW"]), g["probs_W"], rtol=RTOL, atol=0)
+        np.testing.assert_allclose(sm.HeatS(A, g["gW"]), g["heats_W"], rtol=RTOL, atol=0)
+        np.testing.assert_allclose(sm.HybridS(A, g["gW"], 1), g["W_int1"], rtol=RTOL, atol=0)
+
+
+def test_hybrid_transpose_and_rows_topk_exact():
+    from lgcnhs import ops
+    rng = np.random.default_rng(3)
+    n = 77
+    gW = rng.random((n, n))
+    k_item = rng.integers(0, 5, n).astype(np.float64)
+    Wt = ops.hybrid_weight(torch.as_tensor(gW).to(DEV), torch.as_tensor(k_item).to(DEV), 0.3,
+                           transpose=True).cpu().numpy()
+    np.testing.assert_allclose(Wt, O.hybrid_s(np.ones((1, n)) * k_item, gW.T, 0.3), rtol=1e-15)
+    # rows_topk is exact selection: identical to the oracle on the same F, incl. ties
+    F = np.round(rng.random((40, 300)) * 8) / 8  # many exact ties
+    rp, col = O.exclusion_csr(40, 300, (rng.integers(0, 40, 900), rng.integers(0, 300, 900)))
+    from lgcnhs.graph import RowSets
+    ex = RowSets(torch.as_tensor(rp).to(DEV), torch.as_tensor(col).to(DEV), 40, 300)
+    for k in (1, 7, 64, 65, 128):
+        for drop in (True, False):
+            v, i = ops.rows_topk(torch.as_tensor(F).to(DEV), k, ex, drop=drop)
+            ov, oi = O.rows_topk(F, k, rp, col, drop=drop)
+            np.testing.assert_array_equal(i.cpu().numpy(), oi)
+            np.testing.assert_array_equal(v.cpu().numpy(), ov)
+
+
+@pytest.mark.parametrize("tag", ["hybrid", "hybrid85", "probs_ml", "heats_db"])
+def test_recommend_spread_method_vs_reference(golden, tag):
+    import pandas as pd
+    from const import cfg
+    from model.SpreadMethod.recommend import recommendSpreadMethod
+    g = golden("spread_ml100k")
+    U, I, A = _A(g)
+    method, dataset = {"hybrid": ("HybridS", "movielens"), "hybrid85": ("HybridS", "movielens"),
+                       "probs_ml": ("ProbS", "movielens"), "heats_db": ("HeatS", "douban")}[tag]
+    tr = pd.DataFrame({"user_id": g["train"][0].astype(np.int64), "item_id": g["train"][1].astype(np.int64)})
+    va = pd.DataFrame({"user_id": g["val"][0].astype(np.int64), "item_id": g["val"][1].astype(np.int64)})
+    cfg.DATA_SET, cfg.MODEL["name"] = dataset, method
+    cfg.MODEL["HyperParameter"] = {"lambda": float(g[f"{tag}_lambda"])}
+    cfg.RECOMMEND["k"] = int(g["k"])
+    try:
+        recs = recommendSpreadMethod(U, I, tr, va, method)
+    finally:
+        cfg.DATA_SET = "movielens"
+    got = np.array([recs[u] for u in range(U)])
+    gaps = g[f"{tag}_gaps"]
+    compare_topk_sets(got, g[f"{tag}_recs"], gaps, tol=RTOL * np.nanmax(np.abs(gaps)))
+
+
+def test_spread_lightgcn_vs_reference(golden):
+    """The fused LGCNHS path (F blocks x fp32 e0 score inside the top-k kernel) against
+    the reference's getResourceMat + recommendForAllUser (fixture)."""
+    import pandas as pd
+    from model.LightGCN.model import LightGCN
+    from model.SpreadLightGCN.recommend import spread_lightgcn_topk
+    g = golden("lightgcn_mid")
+    U, I, k = int(g["n_users"]), int(g["n_items"]), int(g["k"])
+    torch.manual_seed(42)
+    m = LightGCN(U, I, 64, 3).to(DEV)
+    tr = pd.DataFrame({"user_id": g["train"][0].astype(np.int64), "item_id": g["train"][1].astype(np.int64)})
+    va = pd.DataFrame({"user_id": g["val"][0].astype(np.int64), "item_id": g["val"][1].astype(np.int64)})
+    _, idx = spread_lightgcn_topk(m, U, I, tr, va, float(g["slgcn_lambda"]), k)
+    gaps = g["slgcn_gaps"]
+    compare_topk_sets(idx.cpu().numpy(), g["slgcn_recs"], gaps,
+                      tol=1e-6 * np.nanmax(np.abs(gaps)))
+
+
+def test_dense_api_G_times_F_path(golden):
+    """getAllocateMat-style G (dense, masked) times getHybridSResourceMat F through the
+    numpy API, then recommendForAllUser: same recs as the fused path."""
+    import pandas as pd
+    from model.LightGCN.model import LightGCN
+    from model.SpreadLightGCN.model import allocate_from_model, getHybridSResourceMat
+    from model.SpreadLightGCN.recommend import recommendForAllUser, spread_lightgcn_topk
+    from model.SpreadMethod.model import getSpreadingGeneralMat
+    from utils.graph import convertEdgeIndexToAdjMatrix
+    g = golden("lightgcn_mid")
+    U, I, k = int(g["n_users"]), int(g["n_items"]), int(g["k"])
+    torch.manual_seed(42)
+    m = LightGCN(U, I, 64, 3).to(DEV)
+    trp, vap = g["train"].astype(np.int64), g["val"].astype(np.int64)
+    G = allocate_from_model(m, U, I, convertEdgeIndexToAdjMatrix(U, I, torch.as_tensor(trp)),
+                            convertEdgeIndexToAdjMatrix(U, I, torch.as_tensor(vap))).cpu().numpy()
+    Gref = O.chain_masked_matrix(g["e0_u"], g["e0_i"], *O.exclusion_csr(U, I, trp, vap))
+    assert np.array_equal(G.view(np.uint32), Gref.view(np.uint32))
+    A = O.interaction_matrix(U, I, np.concatenate([trp[0], vap[0]]), np.concatenate([trp[1], vap[1]]))
+    F = getHybridSResourceMat(A, getSpreadingGeneralMat(A), float(g["slgcn_lambda"]))
+    tr = pd.DataFrame({"user_id": trp[0], "item_id": trp[1]})
+    va = pd.DataFrame({"user_id": vap[0], "item_id": vap[1]})
+    recs = recommendForAllUser(G * F, U, tr, va, k)
+    _, idx = spread_lightgcn_topk(m, U, I, tr, va, float(g["slgcn_lambda"]), k)
+    np.testing.assert_array_equal(np.array([recs[u] for u in range(U)]), idx.cpu().numpy())

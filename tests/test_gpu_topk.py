@@ -1,0 +1,121 @@
+"""GPU parity of K2 (e0 scoring + -1024 mask + top-k) and of the dense masked score matrix:
+bit-exact against the C oracle's fp32 fma chain (values AND indices, ties by item id), and
+tie-aware against the reference's own torch.topk results (golden fixtures)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import lgcn_oracle as O
+from _compare import compare_topk_sets
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _excl(U, I, density, seed):
+    rng = np.random.default_rng(seed)
+    n = int(U * I * density)
+    u = rng.integers(0, U, n)
+    i = rng.integers(0, I, n)
+    return O.exclusion_csr(U, I, (u, i))
+
+
+def _rowsets(rp, col, U, I):
+    from lgcnhs.graph import RowSets
+    return RowSets(torch.as_tensor(rp).to(DEV), torch.as_tensor(col).to(DEV), U, I)
+
+
+def _emb(n, d, seed, scale=0.1):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(n, d, generator=g) * scale).float()
+
+
+def test_mfma_chain_is_bit_exact():
+    """score_dense (MFMA 16x16x4 f32) == the C fmaf chain, bit for bit, incl. subnormal-
+    and large-magnitude inputs."""
+    from lgcnhs import ops
+    eu, ei = _emb(37, 64, 1), _emb(53, 64, 2)
+    eu[0, :5] = torch.tensor([1e-39, -3e-40, 1e30, -1e30, 7.0])
+    G = ops.score_dense(eu.to(DEV), ei.to(DEV)).cpu().numpy()
+    ref = O.chain_scores(eu.numpy(), ei.numpy())
+    assert np.array_equal(G.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_score_dense_masked(d):
+    from lgcnhs import ops
+    U, I = 150, 333
+    eu, ei = _emb(U, d, 3), _emb(I, d, 4)
+    rp, col = _excl(U, I, 0.05, 5)
+    G = ops.score_dense(eu.to(DEV), ei.to(DEV), _rowsets(rp, col, U, I)).cpu().numpy()
+    ref = O.chain_masked_matrix(eu.numpy(), ei.numpy(), rp, col)
+    assert np.array_equal(G.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("k", [1, 5, 20, 32, 33, 64, 100, 128])
+def test_score_topk_bit_exact(d, k):
+    from lgcnhs import ops
+    U, I = 301, 2047
+    eu, ei = _emb(U, d, 10 + k), _emb(I, d, 20 + d)
+    rp, col = _excl(U, I, 0.03, k)
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    for ns in (1, None, 7):
+        v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), n_splits=ns)
+        np.testing.assert_array_equal(i.cpu().numpy(), oi)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
+def test_score_topk_edge_cases():
+    from lgcnhs import ops
+    # fewer items than k (padding), all-excluded user (mask values surface), ties (equal
+    # item rows), one user
+    U, I, k = 5, 7, 10
+    eu, ei = _emb(U, 64, 1), _emb(I, 64, 2)
+    ei[3] = ei[1]  # exact ties between items 1 and 3
+    rp, col = O.exclusion_csr(U, I, (np.array([0] * 7 + [2, 2]), np.array(list(range(7)) + [1, 5])))
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    assert (oi[:, 7:] == -1).all() and np.isinf(ov[:, 7:]).all()
+    assert (ov[0] [:7] == -1024.0).all()  # every item of user 0 excluded
+    v1, i1 = ops.score_topk(eu[:1].to(DEV), ei.to(DEV), 3)
+    np.testing.assert_array_equal(i1.cpu().numpy(), O.chain_topk(eu[:1].numpy(), ei.numpy(),
+                                                                  None, None, 3)[1])
+
+
+def test_score_topk_large_catalog_sample():
+    """1M-item catalog (the C5 item count), 256 users: bit-exact vs the C oracle."""
+    from lgcnhs import ops
+    U, I, k = 256, 1_000_000, 20
+    eu, ei = _emb(U, 64, 7), _emb(I, 64, 8)
+    rp, col = _excl(U, I, 1e-4, 9)
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["lightgcn_toy", "lightgcn_edge", "lightgcn_mid",
+                                  "recommend_ml100k"])
+def test_recommend_for_all_user_vs_reference(golden, name):
+    """model.LightGCN.recommend.recommendForAllUser == the reference's dict (fixture),
+    tie-aware at 1e-6, and == the C chain oracle exactly."""
+    from model.LightGCN.model import LightGCN
+    from model.LightGCN.recommend import recommendForAllUser
+    from utils.graph import convertEdgeIndexToAdjMatrix
+    g = golden(name)
+    U, I, k = int(g["n_users"]), int(g["n_items"]), int(g["k"])
+    torch.manual_seed(42)
+    m = LightGCN(U, I, 64, 3).to(DEV)
+    tr = convertEdgeIndexToAdjMatrix(U, I, torch.as_tensor(g["train"].astype(np.int64)))
+    va = convertEdgeIndexToAdjMatrix(U, I, torch.as_tensor(g["val"].astype(np.int64)))
+    recs = recommendForAllUser(m, U, I, tr, va, None, k)
+    got = np.full((U, k), -1)
+    for u, lst in recs.items():
+        got[u, :len(lst)] = lst
+    compare_topk_sets(got, g["recs"], g["rec_gaps"], tol=1e-6)
+    rp, col = O.exclusion_csr(U, I, g["train"], g["val"])
+    _, oi = O.chain_topk(m.users_emb.weight.detach().cpu().numpy(),
+                         m.items_emb.weight.detach().cpu().numpy(), rp, col, k)
+    np.testing.assert_array_equal(got, oi)

@@ -1,0 +1,69 @@
+"""The C-ABI library loads and exports exactly what include/lgcnhs.h declares; argument
+validation rejects bad calls before any launch. CPU only (no kernel runs)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, REPO
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "lgcnhs.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    from lgcnhs import _native as N
+    assert declared_functions() == sorted(N.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    from lgcnhs import _native as N
+    lib = N.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.lg_abi_version() == N.ABI_VERSION
+
+
+def test_argument_validation_without_gpu():
+    from lgcnhs import _native as N
+    lib = N.load_library()
+    z = ctypes.c_void_p(0)
+    one = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    st = lib.lg_spmm_layer_f32(one, one, one, one, z, z, z, z, 10, 0, 48, 0, 1.0, z)
+    assert st == 1 and b"dim" in lib.lg_last_error()
+    st = lib.lg_score_topk_f32(one, one, 4, 4, 64, z, z, -1024.0, 0, 1, one, one, z, 0, z)
+    assert st == 1 and b"k=0" in lib.lg_last_error()
+    st = lib.lg_score_topk_f32(one, one, 4, 4, 64, one, z, -1024.0, 5, 1, one, one, z, 0, z)
+    assert st == 1
+    st = lib.lg_rows_topk_f64(one, 4, 4, 4, z, z, 0, z, z, 7, 3, one, one, z)
+    assert st == 1 and b"excl_mode" in lib.lg_last_error()
+    st = lib.lg_spmm_layer_f32(one, one, one, one, one, z, z, z, 5, 0, 64, 3, 4.0, z)
+    assert st == 1  # LAST needs acc/out
+    assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
+    assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from lgcnhs import _native as N
+    with pytest.raises(RuntimeError, match="not found"):
+        N._lib_backup = N._lib
+        try:
+            N._lib = None
+            N.load_library(str(tmp_path / "nope.so"))
+        finally:
+            N._lib = N._lib_backup
+
+
+def test_product_never_imports_oracle():
+    """The product package must not import, call or link anything under oracle/."""
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")) or f == "Makefile":
+                txt = open(os.path.join(root, f), errors="ignore").read()
+                hit = re.search(r"(import\s+oracle|from\s+oracle|lgcn_oracle|liboracle|"
+                                r"oracle/build|score_chain\.(so|o)\b)", txt)
+                assert not hit, (os.path.join(root, f), hit.group(0))
