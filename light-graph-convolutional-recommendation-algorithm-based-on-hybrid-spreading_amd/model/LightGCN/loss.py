@@ -1,0 +1,43 @@
+"""BPR loss and mini-batch sampling with the reference's interface
+(reference model/LightGCN/loss.py:12-70), sampling on the device."""
+import torch
+
+
+def BPRLoss(users_emb_final, users_emb_0, pos_items_emb_final, pos_items_emb_0,
+            neg_items_emb_final, neg_items_emb_0, lambda_val: float):
+    """reg + bpr with the reference's sign: bpr = -mean(softplus(pos - neg))
+    (reference :12-43)."""
+    reg_loss = lambda_val * (users_emb_0.norm(2).pow(2) + pos_items_emb_0.norm(2).pow(2)
+                             + neg_items_emb_0.norm(2).pow(2))
+    pos_scores = torch.sum(users_emb_final * pos_items_emb_final, dim=-1)
+    neg_scores = torch.sum(users_emb_final * neg_items_emb_final, dim=-1)
+    return -torch.mean(torch.nn.functional.softplus(pos_scores - neg_scores)) + reg_loss
+
+
+def structured_negative_sampling(edge_index: torch.Tensor, num_items: int, generator=None):
+    """(users, pos, neg) with neg uniform over items and (user, neg) not an edge
+    (PyG structured_negative_sampling semantics, rejection on the device; negatives are
+    drawn from the item range)."""
+    u, p = edge_index[0].long(), edge_index[1].long()
+    keys = torch.sort(u * num_items + p).values
+    neg = torch.randint(0, num_items, u.shape, device=u.device, generator=generator)
+    for _ in range(64):
+        q = u * num_items + neg
+        pos = torch.searchsorted(keys, q).clamp_max(keys.numel() - 1)
+        bad = keys[pos] == q
+        if not bool(bad.any()):
+            break
+        neg = torch.where(bad, torch.randint(0, num_items, u.shape, device=u.device,
+                                             generator=generator), neg)
+    return u, p, neg
+
+
+def sampleMiniBatch(batch_size: int, edge_index: torch.Tensor, num_items: int = None,
+                    generator=None):
+    """Reference :46-70: negative-sample every edge, then draw batch_size edges with
+    replacement."""
+    if num_items is None:
+        num_items = int(edge_index[1].max()) + 1
+    u, p, n = structured_negative_sampling(edge_index, num_items, generator)
+    idx = torch.randint(0, u.numel(), (batch_size,), device=u.device, generator=generator)
+    return u[idx], p[idx], n[idx]

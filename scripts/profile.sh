@@ -1,0 +1,17 @@
+# Kernel trace + HBM counters for the bench workload (round-1 profiling recipe).
+# Usage (on the GPU box, from the repo root): bash scripts/profile.sh [extra bench args]
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+ARGS="--no-cpu-baseline $*"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_trace -o run -- \
+  python3 $R/bench.py --steps 5 --warmup 2 $ARGS > $O/prof_trace.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/prof_fetch -o run -- \
+  python3 $R/bench.py --steps 2 --warmup 1 $ARGS > $O/prof_fetch.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/prof_write -o run -- \
+  python3 $R/bench.py --steps 2 --warmup 1 $ARGS > $O/prof_write.log 2>&1
+rc=$?
+echo "profile rc=$rc"
+find $O/prof_trace $O/prof_fetch $O/prof_write -name "*.csv" | head -20
+exit $rc
