@@ -147,11 +147,15 @@ def main():
     t0 = time.time()
     rowptr, src, keys = gen_graph(U, I, E, seed=0, dev=dev)
     nnz = int(src.numel())
-    shard = RowShard(rowptr, src, N, rank, world, dev)
     from lgcnhs import _native as NV
     dis = torch.empty(N, dtype=torch.float32, device=dev)
     NV.check(NV.lib().lg_gcn_norm_f32(NV.ptr(rowptr), N, NV.ptr(dis), NV.stream_handle(dev)),
              "gcn_norm")
+    wgt = torch.empty(nnz, dtype=torch.float32, device=dev)
+    NV.check(NV.lib().lg_gcn_edge_weight_f32(NV.ptr(rowptr), NV.ptr(src), NV.ptr(dis), N, 0,
+                                             NV.ptr(wgt), NV.stream_handle(dev)), "edge weights")
+    shard = RowShard(rowptr, src, N, rank, world, dev, weight=wgt)
+    del wgt
     gen = torch.Generator(device=dev).manual_seed(42)
     e0 = torch.zeros(shard.n_pad, D, device=dev)
     e0[:N] = torch.randn(N, D, device=dev, generator=gen) * 0.1

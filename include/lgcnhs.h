@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 1
+#define LG_ABI_VERSION 2
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -76,7 +76,8 @@ int lg_gcn_edge_weight_f32(const int64_t *rowptr, const int32_t *src, const floa
  * model/LightGCN/model.py:61-63,76-84) and torch.stack/mean (:66-69).
  *
  * For r in [0, n_rows), node g = row_offset + r:
- *   v[g] = sum_{e in row r, s = src[e]} (dis[s] * dis[g]) * x[s]      (ascending s)
+ *   v[g] = sum_{e in row r, s = src[e]} w_e * x[s]      (w_e = w[e], or dis[s]*dis[g]
+ *                                                          when w is NULL; same value)
  *   y[g] = v[g]                                   if y != NULL
  *   acc_mode FIRST: acc[g] = x0[g] + v[g]
  *            MID  : acc[g] = acc[g] + v[g]
@@ -84,7 +85,9 @@ int lg_gcn_edge_weight_f32(const int64_t *rowptr, const int32_t *src, const floa
  *            ONLY : out[g] = (x0[g] + v[g]) / denom            (a 1-layer model)
  *            NONE : nothing
  * x, y, x0, acc, out are [*, dim] arrays indexed by node id g (row-sharded callers pass
- * full-size arrays and their own row range). dim in {32, 64, 128, 256}.
+ * full-size arrays and their own row range). dim in {32, 64, 128, 256}. w (optional) is
+ * the per-entry gcn_norm weight of lg_gcn_edge_weight_f32, indexed like src; passing it
+ * streams 4 B/edge instead of gathering dis[s]. y must not alias x.
  * ------------------------------------------------------------------------------------ */
 enum lg_acc_mode {
   LG_ACC_NONE = 0,
@@ -94,7 +97,7 @@ enum lg_acc_mode {
   LG_ACC_ONLY = 4,
 };
 int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
-                      const float *x, float *y, const float *x0, float *acc, float *out,
+                      const float *w, const float *x, float *y, const float *x0, float *acc, float *out,
                       int64_t n_rows, int64_t row_offset, int32_t dim, int32_t acc_mode,
                       float denom, lg_stream_t stream);
 

@@ -85,20 +85,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
 
-  for (int64_t it = i0; it < i1; it += 16) {
+  auto load_tile = [&](int64_t it, float(&af)[Q]) {
     const int64_t item_l = it + ul;
     const int64_t itc = item_l < n_items ? item_l : n_items - 1;
-    float af[Q];
     load_piece<Q>(ei + itc * D + gq * Q, af);
+  };
 
+  auto do_tile = [&](int64_t it, const float(&af)[Q]) {
     f32x4 acc[NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // s outer / g inner: NG independent accumulation chains interleave on the MFMA pipe
 #pragma unroll
-      for (int s = 0; s < Q; ++s)
+    for (int s = 0; s < Q; ++s)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
-    }
 
     // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r)
 #pragma unroll
@@ -149,6 +151,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
         }
       }
     }
+  };
+
+  // two register buffers: the next tile's item pieces are in flight during this tile's
+  // MFMAs (plain loads, waited by the compiler's counted vmcnt at first use)
+  float afA[Q], afB[Q];
+  if (i0 < i1) load_tile(i0, afA);
+  for (int64_t it = i0; it < i1; it += 32) {
+    const bool has_b = it + 16 < i1;
+    if (has_b) load_tile(it + 16, afB);
+    do_tile(it, afA);
+    if (!has_b) break;
+    if (it + 32 < i1) load_tile(it + 32, afA);
+    do_tile(it + 16, afB);
   }
 
   // final lists

@@ -35,7 +35,7 @@ class RowShard:
     """Rows [r0, r1) of a CSR held by one rank, with rowptr rebased to the local src."""
 
     def __init__(self, rowptr: torch.Tensor, src: torch.Tensor, n_nodes: int, rank: int,
-                 world: int, device=None):
+                 world: int, device=None, weight: torch.Tensor | None = None):
         self.n_nodes, self.rank, self.world = int(n_nodes), rank, world
         self.chunk = math.ceil(self.n_nodes / world)
         self.n_pad = self.chunk * world
@@ -46,6 +46,7 @@ class RowShard:
         e = int(rowptr[self.r1])
         self.rowptr = (rowptr[self.r0:self.r1 + 1] - b).to(dev)
         self.src = src[b:e].to(dev)
+        self.weight = None if weight is None else weight[b:e].to(dev)
         self.nnz = e - b
 
     @property
@@ -56,7 +57,8 @@ class RowShard:
 def hip_layer(shard: RowShard, dis, x, y, x0, acc, out, mode, denom):
     from . import _native as N
     N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(shard.rowptr), N.ptr(shard.src), N.ptr(dis), N.ptr(x), N.ptr(y), N.ptr(x0),
+        N.ptr(shard.rowptr), N.ptr(shard.src), N.ptr(dis), N.ptr(shard.weight), N.ptr(x),
+        N.ptr(y), N.ptr(x0),
         N.ptr(acc), N.ptr(out), shard.n_rows, shard.r0, x.shape[1], mode, float(denom),
         N.stream_handle(x.device)), "lg_spmm_layer_f32")
 

@@ -28,16 +28,16 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------ propagation
 def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
-               row_begin: int = 0, row_end: int | None = None, dis=None,
-               rowptr=None, src=None) -> None:
-    """One lg_spmm_layer_f32 launch over rows [row_begin, row_end) of ``adj``."""
+               row_begin: int = 0, row_end: int | None = None,
+               stream_weights: bool = True) -> None:
+    """One lg_spmm_layer_f32 launch over rows [row_begin, row_end) of ``adj``; with
+    stream_weights the precomputed gcn_norm edge weights are streamed (else recomputed
+    from dis; identical values)."""
     if row_end is None:
         row_end = adj.n_nodes
-    rp = adj.rowptr if rowptr is None else rowptr
-    sr = adj.src if src is None else src
-    ds = adj.dis() if dis is None else dis
+    w = adj.edge_weight() if stream_weights else None
     N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(rp[row_begin:] if rowptr is None else rp), N.ptr(sr), N.ptr(ds), N.ptr(x),
+        N.ptr(adj.rowptr[row_begin:]), N.ptr(adj.src), N.ptr(adj.dis()), N.ptr(w), N.ptr(x),
         N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), row_end - row_begin, row_begin,
         x.shape[1], mode, float(denom), N.stream_handle(x.device)), "lg_spmm_layer_f32")
 

@@ -147,6 +147,9 @@ def test_large_graph_properties():
     y = torch.empty_like(x)
     from lgcnhs import _native as N
     ops.spmm_layer(adj, x, y, None, None, None, N.LG_ACC_NONE, 1.0)
+    y2 = torch.empty_like(x)
+    ops.spmm_layer(adj, x, y2, None, None, None, N.LG_ACC_NONE, 1.0, stream_weights=False)
+    assert torch.equal(y, y2)  # streamed weights == recomputed dis[s]*dis[g], bitwise
     rowptr, src, dis = adj.rowptr.cpu().numpy(), adj.src.cpu().numpy(), adj.dis().cpu().numpy()
     xc = x.cpu().numpy().astype(np.float64)
     yc = y.cpu().numpy()
