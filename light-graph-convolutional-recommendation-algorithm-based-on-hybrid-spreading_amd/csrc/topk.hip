@@ -16,9 +16,10 @@
 // Top-K: per user a candidate list of CAP entries in LDS; a score enters only if it beats
 // the user's current K-th best (tau), so after the first few hundred items almost nothing
 // enters and the VALU cost per score is one compare. The exclusion row (sorted) is
-// binary-searched only for entering candidates: an excluded item takes mask_value (-1024)
-// and is re-tested, which is exactly the reference's masked top-k. Lists are compacted by
-// the wave-wide bitonic sort of common.h. Order: (score desc, item asc).
+// binary-searched only for list entries, in batch when the list is compacted: an excluded
+// item takes mask_value (-1024) before the sort, which is exactly the reference's masked
+// top-k. Lists are compacted by the wave-wide bitonic sort of common.h. Order: (score
+// desc, item asc). The main loop thus issues no global load but the item tiles.
 #include "common.h"
 
 namespace lg {
@@ -36,6 +37,27 @@ __device__ __forceinline__ void load_piece(const float *__restrict__ p, float (&
     v[4 * t + 2] = q.z;
     v[4 * t + 3] = q.w;
   }
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// Item-tile loads hidden from the compiler's wait analysis (cdna_hip_programming.md §5.7
+// item 1): the compiler's loop merge otherwise waits for the prefetch it just issued. The
+// caller waits by hand with wait_vm<N>() = "all but the N youngest vector-memory ops".
+template <int Q>
+__device__ __forceinline__ void asm_load_piece(const float *p, f32x4v (&v)[Q / 4]) {
+#pragma unroll
+  for (int t = 0; t < Q / 4; ++t)
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2"
+                 : "=v"(v[t])
+                 : "v"(p), "i"(t * 16)
+                 : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (§5.4 rule 18)
 }
 
 // One wave: NG groups of 16 users; the block's waves work independently.
@@ -66,7 +88,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   float uf[NG][Q];
   bool uvalid[NG];
   int64_t ex_lo[NG], ex_hi[NG];
-  int cnt[NG];
+  int cnt[NG], chk[NG];
   float tau[NG];
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
@@ -81,17 +103,47 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       ex_hi[g] = ex_rowptr[u + 1];
     }
     cnt[g] = 0;
+    chk[g] = 0;
     tau[g] = neg_inf<float>();
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
 
-  auto load_tile = [&](int64_t it, float(&af)[Q]) {
-    const int64_t item_l = it + ul;
-    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
-    load_piece<Q>(ei + itc * D + gq * Q, af);
+  // Exclusion is applied lazily: a candidate enters on its raw score (or on the mask value
+  // when that alone beats tau), and entries [chk, n) of a list are binary-searched in the
+  // user's sorted exclusion row only when the list is compacted. Exact: an excluded item
+  // would enter with mask_value, and mask_value > tau admits every item.
+  auto compact_user = [&](int g, int u) {
+    const int n = __shfl(cnt[g], u);
+    const int c0 = __shfl(chk[g], u);
+    const int64_t lo = __shfl(ex_lo[g], u);
+    const int64_t hi = __shfl(ex_hi[g], u);
+    float *ks = &cs[wave][g][u][0];
+    int *is = &ci[wave][g][u][0];
+    if (lo < hi) {
+      for (int e = c0 + lane; e < n; e += 64) {
+        const int32_t item = is[e];
+        const int64_t p = lower_bound_i32(ex_col, lo, hi, item);
+        if (p < hi && ex_col[p] == item) ks[e] = mask_value;
+      }
+      wave_sync();
+    }
+    float t;
+    int tid;
+    const int nc = wave_compact<float, M>(ks, is, n, k, t, tid);
+    if (ul == u) {
+      cnt[g] = nc;
+      chk[g] = nc;
+      tau[g] = t;
+    }
   };
 
-  auto do_tile = [&](int64_t it, const float(&af)[Q]) {
+  auto load_tile = [&](int64_t it, f32x4v(&af)[Q / 4]) {
+    const int64_t item_l = it + ul;
+    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
+    asm_load_piece<Q>(ei + itc * D + gq * Q, af);
+  };
+
+  auto do_tile = [&](int64_t it, const f32x4v(&af)[Q / 4]) {
     f32x4 acc[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -100,26 +152,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     for (int s = 0; s < Q; ++s)
 #pragma unroll
       for (int g = 0; g < NG; ++g)
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s / 4][s % 4], uf[g][s], acc[g], 0,
+                                                      0, 0);
 
     // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r)
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
+      const bool mask_enters = mask_value > tau[g];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t item = it + gq * 4 + r;
-        float sc = acc[g][r];
-        bool cand = uvalid[g] && item < i1 && sc > tau[g];
-        if (__ballot(cand)) {
-          if (cand && ex_lo[g] < ex_hi[g]) {
-            const int64_t p = lower_bound_i32(ex_col, ex_lo[g], ex_hi[g], (int32_t)item);
-            ex_lo[g] = p;  // this lane's later items are larger
-            if (p < ex_hi[g] && ex_col[p] == (int32_t)item) {
-              sc = mask_value;
-              cand = sc > tau[g];
-            }
-          }
-          const uint64_t bal = __ballot(cand);
+        const float sc = acc[g][r];
+        const bool cand = uvalid[g] && item < i1 && (sc > tau[g] || mask_enters);
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
           const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
           if (cand) {
             cs[wave][g][ul][pos] = sc;
@@ -130,41 +176,53 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       }
     }
 
-    // compact every user whose list could overflow on the next tile (+16 max per tile)
+  };
+
+  // compact every user whose list could overflow before the next check (+32 max: two
+  // 16-item tiles per loop iteration)
+  auto maybe_compact = [&]() {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+      uint64_t need = __ballot(cnt[g] > CAP - 32) & 0xffffull;
       if (need) {
         wave_sync();
         while (need) {
           const int u = __ffsll((long long)need) - 1;
           need &= need - 1;
-          const int n = __shfl(cnt[g], u);
-          float t;
-          int tid;
-          const int nc = wave_compact<float, M>(&cs[wave][g][u][0], &ci[wave][g][u][0], n, k,
-                                                t, tid);
-          if (ul == u) {
-            cnt[g] = nc;
-            tau[g] = t;
-          }
+          compact_user(g, u);
         }
       }
     }
   };
 
-  // two register buffers: the next tile's item pieces are in flight during this tile's
-  // MFMAs (plain loads, waited by the compiler's counted vmcnt at first use)
-  float afA[Q], afB[Q];
+  // Two register buffers: the next tile's item pieces are in flight during this tile's
+  // MFMAs. The loads are inline asm (invisible to the compiler's waits), so every use is
+  // preceded by a hand-counted wait: LT = loads per tile; before computing tile t the only
+  // younger loads allowed in flight are tile t+1's.
+  constexpr int LT = Q / 4;
+  f32x4v afA[LT], afB[LT];
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the prologue loads: vmcnt(0)
   if (i0 < i1) load_tile(i0, afA);
   for (int64_t it = i0; it < i1; it += 32) {
     const bool has_b = it + 16 < i1;
-    if (has_b) load_tile(it + 16, afB);
+    if (has_b) {
+      load_tile(it + 16, afB);
+      wait_vm<LT>();
+    } else {
+      wait_vm<0>();
+    }
     do_tile(it, afA);
     if (!has_b) break;
-    if (it + 32 < i1) load_tile(it + 32, afA);
+    if (it + 32 < i1) {
+      load_tile(it + 32, afA);
+      wait_vm<LT>();
+    } else {
+      wait_vm<0>();
+    }
     do_tile(it + 16, afB);
+    maybe_compact();
   }
+  wait_vm<0>();
 
   // final lists
   wave_sync();
@@ -173,11 +231,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     for (int u = 0; u < 16; ++u) {
       const int64_t user = ubase + g * 16 + u;
       if (user >= n_users) break;
-      const int n = __shfl(cnt[g], u);
-      float t;
-      int tid;
-      const int nc =
-          wave_compact<float, M>(&cs[wave][g][u][0], &ci[wave][g][u][0], n, k, t, tid);
+      compact_user(g, u);
+      const int nc = __shfl(cnt[g], u);
       for (int e = lane; e < k; e += 64) {
         const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
         const int id = e < nc ? ci[wave][g][u][e] : -1;

@@ -1,16 +1,22 @@
-"""Row-sharded multi-GPU propagation: one process per GPU, RCCL all-gather over xGMI.
+"""Row-sharded multi-GPU propagation: one process per GPU, RCCL all-gather over xGMI,
+overlapped with the SpMM.
 
-SURVEY.md §8(e): the N = U+I rows of A_hat are split into `world` contiguous ranges of
-`chunk = ceil(N / world)` rows; rank r owns rows [r*chunk, (r+1)*chunk) of the CSR and
-of every embedding buffer. Each rank keeps a full (padded) replica of the layer input x;
-per layer it runs the SpMM kernel on its own rows, writing them into its slice of the next
-layer's buffer, then ``all_gather_into_tensor`` rebuilds the full buffer on every rank
-(the only exchange step of the path). The layer-mean accumulator stays local. Equal row
-counts keep node ids unchanged (no relabelling); the uniform synthetic graphs of the
-benchmark are nnz-balanced under equal row counts.
+SURVEY.md §8(e). Rank r owns the contiguous original rows [r*C*S, (r+1)*C*S) of A_hat
+(equal row counts; the benchmark's uniform graphs are nnz-balanced that way), cut into C
+sub-chunks of S rows. Every rank keeps a full replica of the layer input x. Per layer it
+runs the SpMM kernel on one sub-chunk at a time and, as soon as sub-chunk c is done,
+starts an asynchronous ``all_gather_into_tensor`` of it (RCCL runs on its own stream)
+while the kernel works on sub-chunk c+1; the next layer waits for all C gathers. Only the
+last gather of a layer is exposed.
 
-The per-shard layer is pluggable so that the bookkeeping can be exercised on CPU with
-the gloo backend (tests/test_dist_gloo.py); on GPUs it is lg_spmm_layer_f32.
+For the gathers to land in place, node ids live in a *chunk-major* layout:
+    new(g) = c*(W*S) + r*S + i      for original g = r*(C*S) + c*S + i
+so sub-chunk c of every rank is one contiguous block of W*S rows in rank order, which is
+exactly what ``all_gather_into_tensor`` writes. ``src`` ids, dis and e0 are permuted into
+that layout once; the output is permuted back on demand. C = 1 is the plain row shard.
+
+The per-shard layer is pluggable so the bookkeeping can run on CPU with gloo
+(tests/test_dist_gloo.py); on GPUs it is lg_spmm_layer_f32.
 """
 from __future__ import annotations
 
@@ -32,54 +38,82 @@ def acc_mode(l: int, layers: int) -> int:
 
 
 class RowShard:
-    """Rows [r0, r1) of a CSR held by one rank, with rowptr rebased to the local src."""
+    """This rank's rows of a CSR over n_nodes nodes, in the chunk-major layout."""
 
     def __init__(self, rowptr: torch.Tensor, src: torch.Tensor, n_nodes: int, rank: int,
-                 world: int, device=None, weight: torch.Tensor | None = None):
-        self.n_nodes, self.rank, self.world = int(n_nodes), rank, world
-        self.chunk = math.ceil(self.n_nodes / world)
-        self.n_pad = self.chunk * world
-        self.r0 = min(rank * self.chunk, self.n_nodes)
-        self.r1 = min(self.n_nodes, self.r0 + self.chunk)
+                 world: int, device=None, weight: torch.Tensor | None = None,
+                 chunks: int = 1):
+        self.n_nodes, self.rank, self.world, self.chunks = int(n_nodes), rank, world, chunks
+        self.S = math.ceil(self.n_nodes / (world * chunks))
+        self.n_pad = self.S * world * chunks
         dev = device if device is not None else rowptr.device
-        b = int(rowptr[self.r0])
-        e = int(rowptr[self.r1])
-        self.rowptr = (rowptr[self.r0:self.r1 + 1] - b).to(dev)
-        self.src = src[b:e].to(dev)
+        self.device = dev
+        g0 = min(rank * chunks * self.S, self.n_nodes)
+        g1 = min(self.n_nodes, g0 + chunks * self.S)
+        b, e = int(rowptr[g0]), int(rowptr[g1])
+        self.g0, self.g1 = g0, g1
+        self.rowptr = (rowptr[g0:g1 + 1] - b).to(dev)
+        src_local = src[b:e].to(dev)
+        self.src = self.to_layout(src_local.to(torch.int64)).to(torch.int32) if (world > 1 or chunks > 1) else src_local
         self.weight = None if weight is None else weight[b:e].to(dev)
         self.nnz = e - b
+        # (local row begin, local row end, output row offset) per sub-chunk
+        self.pieces = []
+        for c in range(chunks):
+            lb = min(c * self.S, g1 - g0)
+            le = min((c + 1) * self.S, g1 - g0)
+            self.pieces.append((lb, le, c * world * self.S + rank * self.S))
 
     @property
     def n_rows(self) -> int:
-        return self.r1 - self.r0
+        return self.g1 - self.g0
+
+    # ------------------------------------------------------------------ layout maps
+    def to_layout(self, g: torch.Tensor) -> torch.Tensor:
+        """original node id -> chunk-major id."""
+        CS = self.chunks * self.S
+        r, o = g // CS, g % CS
+        c, i = o // self.S, o % self.S
+        return c * (self.world * self.S) + r * self.S + i
+
+    def permute_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """[n_nodes, ...] in original order -> [n_pad, ...] chunk-major (zero padding)."""
+        out = torch.zeros((self.n_pad,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        out[self.to_layout(torch.arange(self.n_nodes, device=t.device))] = t
+        return out
+
+    def unpermute_rows(self, t: torch.Tensor) -> torch.Tensor:
+        return t[self.to_layout(torch.arange(self.n_nodes, device=t.device))]
 
 
-def hip_layer(shard: RowShard, dis, x, y, x0, acc, out, mode, denom):
+def hip_layer(shard: RowShard, piece, dis, x, y, x0, acc, out, mode, denom):
     from . import _native as N
+    lb, le, off = piece
+    if le <= lb:
+        return
+    w = None if shard.weight is None else shard.weight
     N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(shard.rowptr), N.ptr(shard.src), N.ptr(dis), N.ptr(shard.weight), N.ptr(x),
-        N.ptr(y), N.ptr(x0),
-        N.ptr(acc), N.ptr(out), shard.n_rows, shard.r0, x.shape[1], mode, float(denom),
-        N.stream_handle(x.device)), "lg_spmm_layer_f32")
+        N.ptr(shard.rowptr[lb:]), N.ptr(shard.src), N.ptr(dis), N.ptr(w), N.ptr(x),
+        N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), le - lb, off, x.shape[1], mode,
+        float(denom), N.stream_handle(x.device)), "lg_spmm_layer_f32")
 
 
-def all_gather_rows(buf: torch.Tensor, shard: RowShard, group=None) -> None:
-    """Rebuild the full [n_pad, d] buffer from every rank's [chunk, d] slice, in place."""
-    c = shard.chunk
-    mine = buf[shard.rank * c:(shard.rank + 1) * c]
+def _gather_block(buf: torch.Tensor, shard: RowShard, c: int, group=None, async_op=True):
+    W, S = shard.world, shard.S
+    blk = buf[c * W * S:(c + 1) * W * S]
+    mine = blk[shard.rank * S:(shard.rank + 1) * S]
     if dist.get_backend(group) == "gloo":
-        dist.all_gather([buf[r * c:(r + 1) * c] for r in range(shard.world)], mine.clone(),
-                        group=group)
-    else:
-        dist.all_gather_into_tensor(buf, mine, group=group)
+        return dist.all_gather([blk[r * S:(r + 1) * S] for r in range(W)], mine.clone(),
+                               group=group, async_op=async_op)
+    return dist.all_gather_into_tensor(blk, mine, group=group, async_op=async_op)
 
 
 class ShardedPropagation:
-    """mean_{l<=L} A_hat^l e0 for this rank's rows, with a per-layer all-gather."""
+    """mean_{l<=L} A_hat^l e0 on this rank's rows, all-gathers overlapped with the SpMM."""
 
-    def __init__(self, shard: RowShard, dis: torch.Tensor, dim: int, layers: int,
+    def __init__(self, shard: RowShard, dis_layout: torch.Tensor, dim: int, layers: int,
                  device, layer_fn=hip_layer, group=None):
-        self.shard, self.dis, self.layers, self.group = shard, dis, layers, group
+        self.shard, self.dis, self.layers, self.group = shard, dis_layout, layers, group
         self.layer_fn = layer_fn
         n_pad = shard.n_pad
         self.bufs = [torch.zeros(n_pad, dim, device=device),
@@ -87,25 +121,34 @@ class ShardedPropagation:
         self.out = torch.zeros(n_pad, dim, device=device)
         self.events = None  # optional list of (start, end) event pairs around each layer
 
-    def forward(self, e0: torch.Tensor, gather_out: bool = False) -> torch.Tensor:
-        """e0: full [n_pad, d] layer-0 embeddings (replicated). Returns the [n_pad, d]
-        output buffer; rows outside this rank's range are valid only with gather_out."""
-        x = e0
+    def forward(self, e0_layout: torch.Tensor, gather_out: bool = False) -> torch.Tensor:
+        """e0_layout: [n_pad, d] layer-0 embeddings in the chunk-major layout (replicated).
+        Returns the [n_pad, d] output (chunk-major); rows of other ranks are valid only
+        with gather_out."""
+        sh = self.shard
+        x = e0_layout
         L = self.layers
         for l in range(L):
             last = l == L - 1
             y = None if last else self.bufs[l % 2]
+            mode = acc_mode(l, L)
+            handles = []
             if self.events is not None:
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s = torch.cuda.Event(enable_timing=True)
                 s.record()
-            self.layer_fn(self.shard, self.dis, x, y, e0, self.out, self.out,
-                          acc_mode(l, L), L + 1)
+            for c, piece in enumerate(sh.pieces):
+                self.layer_fn(sh, piece, self.dis, x, y, e0_layout, self.out, self.out, mode,
+                              L + 1)
+                if not last and sh.world > 1:
+                    handles.append(_gather_block(y, sh, c, self.group))
             if self.events is not None:
+                e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 self.events.append((s, e))
-            if not last and self.shard.world > 1:
-                all_gather_rows(y, self.shard, self.group)
+            for h in handles:
+                h.wait()
             x = y
-        if gather_out and self.shard.world > 1:
-            all_gather_rows(self.out, self.shard, self.group)
+        if gather_out and sh.world > 1:
+            for c in range(sh.chunks):
+                _gather_block(self.out, sh, c, self.group, async_op=False)
         return self.out

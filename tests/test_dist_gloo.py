@@ -22,12 +22,14 @@ def _free_port():
     return p
 
 
-def cpu_layer(shard, dis, x, y, x0, acc, out, mode, denom):
-    """Oracle stand-in for lg_spmm_layer_f32 over the shard's rows."""
+def cpu_layer(shard, piece, dis, x, y, x0, acc, out, mode, denom):
+    """Oracle stand-in for lg_spmm_layer_f32 over one sub-chunk of the shard's rows (all
+    ids in the chunk-major layout)."""
+    lb, le, off = piece
     rp = shard.rowptr.numpy()
     src = shard.src.numpy().astype(np.int64)
-    for r in range(shard.n_rows):
-        g = shard.r0 + r
+    for r in range(lb, le):
+        g = off + (r - lb)
         s = src[rp[r]:rp[r + 1]]
         w = dis[s] * dis[g]
         v = (w[:, None] * x[s]).sum(0) if s.size else torch.zeros(x.shape[1])
@@ -43,7 +45,7 @@ def cpu_layer(shard, dis, x, y, x0, acc, out, mode, denom):
             out[g] = (x0[g] + v) / denom
 
 
-def _worker(rank, world, port, U, I, users, items, layers, q):
+def _worker(rank, world, port, U, I, users, items, layers, chunks, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,26 +59,27 @@ def _worker(rank, world, port, U, I, users, items, layers, q):
         deg = (rowptr[1:] - rowptr[:-1]).float()
         dis = deg.pow(-0.5)
         dis.masked_fill_(dis == float("inf"), 0)
-        shard = RowShard(rowptr, src, n, rank, world, "cpu")
+        shard = RowShard(rowptr, src, n, rank, world, "cpu", chunks=chunks)
         torch.manual_seed(0)
-        e0 = torch.zeros(shard.n_pad, 8)
-        e0[:n] = torch.randn(n, 8) * 0.1
-        prop = ShardedPropagation(shard, dis, 8, layers, "cpu", layer_fn=cpu_layer)
+        e0 = shard.permute_rows(torch.randn(n, 8) * 0.1)
+        prop = ShardedPropagation(shard, shard.permute_rows(dis), 8, layers, "cpu",
+                                  layer_fn=cpu_layer)
         out = prop.forward(e0, gather_out=True)
         if rank == 0:
-            q.put(out[:n].numpy().copy())
+            q.put(shard.unpermute_rows(out).numpy().copy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,layers", [(2, 3), (2, 1), (3, 2)])
-def test_sharded_propagation_gloo(world, layers):
+@pytest.mark.parametrize("world,layers,chunks", [(2, 3, 1), (2, 1, 1), (3, 2, 1), (2, 3, 3),
+                                                (3, 3, 2), (1, 3, 4)])
+def test_sharded_propagation_gloo(world, layers, chunks):
     U, I = 13, 17
     users, items = O.coo_to_interactions(U, I, O.coo_adjacency(U, I, *np.random.default_rng(1).integers(0, [U, I], (60, 2)).T))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, U, I, users, items, layers, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, U, I, users, items, layers, chunks, q))
              for r in range(world)]
     for p in procs:
         p.start()
