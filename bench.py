@@ -176,7 +176,7 @@ def main():
     if cpu_src is None:
         del src
     torch.cuda.synchronize()
-    log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {shard.r0}-{shard.r1} "
+    log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {shard.g0}-{shard.g1} "
         f"setup {time.time() - t0:.1f}s")
 
     for _ in range(args.warmup):

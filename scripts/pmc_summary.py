@@ -1,0 +1,57 @@
+"""Summarise rocprofv3 kernel-trace + PMC passes (scripts/profile.sh output) into
+profiles/: per-kernel average duration, FETCH_SIZE / WRITE_SIZE per launch and the HBM
+traffic estimate bench.py reports as roofline.traffic.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts half the bytes of
+16-B-per-lane streaming/gather reads -> x2; WRITE_SIZE (KiB) is exact for 16-B stores."""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"k_spmm_layer": "lg_spmm_layer_f32", "k_score_topk": "lg_score_topk_f32",
+        "k_topk_merge": "lg_score_topk_f32(merge)"}
+
+
+def kernel_key(name):
+    for k, v in KEYS.items():
+        if k in name:
+            return v
+    return None
+
+
+def main(out_dir, tag, workload="c5-d64", world=1):
+    g = os.path.join(REPO, "gpurun_out")
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(g, "prof_trace", "run_kernel_stats.csv"))):
+        k = kernel_key(r["Name"])
+        if k:
+            stats[k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                        "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
+    ctr = defaultdict(list)
+    for sub in ("prof_fetch", "prof_write"):
+        for r in csv.DictReader(open(os.path.join(g, sub, "run_counter_collection.csv"))):
+            k = kernel_key(r["Kernel_Name"])
+            if k:
+                ctr[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (k, c), v in ctr.items():
+        stats.setdefault(k, {})[c + "_KiB_per_launch"] = sum(v) / len(v)
+    for k, s in stats.items():
+        if "FETCH_SIZE_KiB_per_launch" in s and "WRITE_SIZE_KiB_per_launch" in s:
+            s["hbm_bytes_per_launch"] = (2 * s["FETCH_SIZE_KiB_per_launch"]
+                                         + s["WRITE_SIZE_KiB_per_launch"]) * 1024
+    os.makedirs(out_dir, exist_ok=True)
+    json.dump(stats, open(os.path.join(out_dir, f"{tag}_kernel_summary.json"), "w"), indent=1)
+    tp = os.path.join(out_dir, "pmc_traffic.json")
+    d = json.load(open(tp)) if os.path.exists(tp) else {}
+    if "lg_spmm_layer_f32" in stats and "hbm_bytes_per_launch" in stats["lg_spmm_layer_f32"]:
+        d[f"{workload}/n{world}"] = {"kernel": "lg_spmm_layer_f32", "source": tag,
+                                     **stats["lg_spmm_layer_f32"]}
+    json.dump(d, open(tp, "w"), indent=1)
+    print(json.dumps(stats, indent=1))
+
+
+if __name__ == "__main__":
+    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r01")

@@ -26,9 +26,10 @@ def test_gcn_norm_weights_match_reference(golden, name):
     # the fixture COO is (row=source, col=target) sorted by row; the CSR is target-major.
     coo = g["train_coo"].astype(np.int64)
     order = np.lexsort((coo[0], coo[1]))  # by (target, source)
-    # torch-CPU pow(-0.5) is a vectorised rsqrt approximation (differs from 1/sqrt in the
-    # last bit for ~0.5% of degrees); the kernel computes IEEE 1/sqrt: <= 1 ulp apart.
-    np.testing.assert_array_max_ulp(w, g["gcn_w"][order], maxulp=1)
+    # torch-CPU pow(-0.5) is a vectorised rsqrt (differs from IEEE 1/sqrt in the last bit
+    # for ~0.5% of degrees, CPU-ISA dependent); the kernel computes 1/sqrt, so each dis is
+    # <= 1 ulp off and the product dis[s]*dis[t] <= 3 ulp.
+    np.testing.assert_array_max_ulp(w, g["gcn_w"][order], maxulp=3)
 
 
 @pytest.mark.parametrize("name", ["lightgcn_toy", "lightgcn_edge", "lightgcn_mid"])
