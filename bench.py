@@ -107,6 +107,35 @@ def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
                       f"{e_end} directed nnz x {layers} layers, full {n}x{dim} x, median of 3"}
 
 
+def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
+    """Time `steps` full L-layer forwards; returns (max-over-ranks seconds, average SpMM
+    'launch' seconds = one layer's kernels on this rank, from HIP events on the stream)."""
+    from lgcnhs.dist import ShardedPropagation
+    e0 = shard.permute_rows(e0_orig)  # chunk-major layout (identity at N=1)
+    prop = ShardedPropagation(shard, dis_l, D, L, dev)
+    for _ in range(warmup):
+        prop.forward(e0)
+    torch.cuda.synchronize()
+    prop.events = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        prop.forward(e0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    kernel_ms = [s.elapsed_time(e) for s, e in prop.events]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    del prop, e0
+    return elapsed, sum(kernel_ms) / len(kernel_ms) / 1e3
+
+
 def load_traffic(workload, world):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -130,6 +159,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
+    ap.add_argument("--extra-dims", type=int, nargs="*", default=[128],
+                    help="also time the same graph at these embedding widths")
     ap.add_argument("--chunks", type=int, default=0,
                     help="sub-chunks per rank per layer for comm/compute overlap (0 = auto)")
     args = ap.parse_args()
@@ -149,7 +180,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from lgcnhs import ops
-    from lgcnhs.dist import RowShard, ShardedPropagation
+    from lgcnhs.dist import RowShard
     from lgcnhs.graph import RowSets
 
     U, I, E, D, L = WORKLOADS[args.workload]
@@ -167,10 +198,9 @@ def main():
     chunks = args.chunks if args.chunks else (1 if world == 1 else 4)
     shard = RowShard(rowptr, src, N, rank, world, dev, weight=wgt, chunks=chunks)
     del wgt
+    dis_l = shard.permute_rows(dis)
     gen = torch.Generator(device=dev).manual_seed(42)
     e0_orig = torch.randn(N, D, device=dev, generator=gen) * 0.1
-    e0 = shard.permute_rows(e0_orig)  # chunk-major layout (identity at N=1)
-    prop = ShardedPropagation(shard, shard.permute_rows(dis), D, L, dev)
     cpu_rp, cpu_src = (rowptr, src) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else (None, None)
     del rowptr
     if cpu_src is None:
@@ -179,34 +209,30 @@ def main():
     log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {shard.g0}-{shard.g1} "
         f"setup {time.time() - t0:.1f}s")
 
-    for _ in range(args.warmup):
-        prop.forward(e0)
-    torch.cuda.synchronize()
-    prop.events = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        prop.forward(e0)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t1
-    kernel_ms = [s.elapsed_time(e) for s, e in prop.events]
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # one "launch" = one layer's SpMM over this rank's rows (1 kernel at N=1, `chunks`
-    # kernels back to back on the compute stream at N>1)
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    elapsed, avg_kernel_s = time_propagation(shard, dis_l, e0_orig, D, L, args.steps,
+                                             args.warmup, world, dev)
     edge_layers = nnz * L * args.steps
     value = edge_layers / elapsed
     # algorithmic bytes per SpMM launch: nnz*(8+4d) + rows*(4+4d)
     alg_bytes = shard.nnz * (8 + 4 * D) + shard.n_rows * (4 + 4 * D)
     achieved = alg_bytes / avg_kernel_s / 1e9
     traffic = load_traffic(args.workload, world)
+
+    # the same graph at the other embedding widths the configs name (C5: d=128)
+    extra = {}
+    for d2 in args.extra_dims:
+        if d2 == D:
+            continue
+        e2 = torch.randn(N, d2, device=dev, generator=gen) * 0.1
+        el2, k2 = time_propagation(shard, dis_l, e2, d2, L, max(2, args.steps // 2), 1, world,
+                                   dev)
+        b2 = shard.nnz * (8 + 4 * d2) + shard.n_rows * (4 + 4 * d2)
+        extra[f"d{d2}"] = {"value": nnz * L * max(2, args.steps // 2) / el2,
+                           "unit": "edge-layers/s", "ms_per_step": el2 / max(2, args.steps // 2) * 1e3,
+                           "roofline_frac": b2 / k2 / 1e9 / HBM_PEAK_GBS,
+                           "achieved_GBs": b2 / k2 / 1e9}
+        del e2
+        torch.cuda.empty_cache()
 
     topk = None
     if not args.no_topk:
@@ -259,6 +285,7 @@ def main():
                          "avg_launch_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes},
             "topk": topk,
+            "other_dims": extra,
             "cpu_baseline": cpu,
             "host": platform.node(),
         }

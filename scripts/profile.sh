@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
-ARGS="--no-cpu-baseline $*"
+ARGS="--no-cpu-baseline --extra-dims $*"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_trace -o run -- \
   python3 $R/bench.py --steps 5 --warmup 2 $ARGS > $O/prof_trace.log 2>&1 &&
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/prof_fetch -o run -- \
