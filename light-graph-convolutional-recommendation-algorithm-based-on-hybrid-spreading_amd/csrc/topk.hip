@@ -89,7 +89,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   bool uvalid[NG];
   int64_t ex_lo[NG], ex_hi[NG];
   int cnt[NG], chk[NG];
-  float tau[NG];
+  float tau[NG], thr[NG];
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int64_t u = ubase + g * 16 + ul;
@@ -105,6 +105,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     cnt[g] = 0;
     chk[g] = 0;
     tau[g] = neg_inf<float>();
+    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
 
@@ -134,6 +135,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       cnt[g] = nc;
       chk[g] = nc;
       tau[g] = t;
+      // a masked (excluded) item would enter with mask_value: admit everything then
+      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
     }
   };
 
@@ -155,15 +158,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s / 4][s % 4], uf[g][s], acc[g], 0,
                                                       0, 0);
 
-    // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r)
+    // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r). Fast path: one max
+    // and one compare per group against thr = the entry threshold (tau, or -inf while the
+    // mask value itself would enter, +inf for padding users); the exact per-score test
+    // runs only when some lane of the wave has a candidate.
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const bool mask_enters = mask_value > tau[g];
+      const float m = fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
+      if (__ballot(m > thr[g]) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t item = it + gq * 4 + r;
         const float sc = acc[g][r];
-        const bool cand = uvalid[g] && item < i1 && (sc > tau[g] || mask_enters);
+        const bool cand = item < i1 && sc > thr[g];
         const uint64_t bal = __ballot(cand);
         if (bal) {
           const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
@@ -175,7 +182,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
         }
       }
     }
-
   };
 
   // compact every user whose list could overflow before the next check (+32 max: two
