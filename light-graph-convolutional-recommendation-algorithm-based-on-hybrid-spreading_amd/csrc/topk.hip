@@ -20,6 +20,8 @@
 // item takes mask_value (-1024) before the sort, which is exactly the reference's masked
 // top-k. Lists are compacted by the wave-wide bitonic sort of common.h. Order: (score
 // desc, item asc). The main loop thus issues no global load but the item tiles.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace lg {
@@ -61,7 +63,7 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // One wave: NG groups of 16 users; the block's waves work independently.
-template <int D, int NG, int M, int WAVES>
+template <int D, int NG, int M, int WAVES, int PF>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
     int64_t n_items, const int64_t *__restrict__ ex_rowptr,
@@ -184,12 +186,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   };
 
-  // compact every user whose list could overflow before the next check (+32 max: two
-  // 16-item tiles per loop iteration)
+  // compact every user whose list could overflow on the next tile (+16 max per tile)
   auto maybe_compact = [&]() {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      uint64_t need = __ballot(cnt[g] > CAP - 32) & 0xffffull;
+      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
       if (need) {
         wave_sync();
         while (need) {
@@ -201,32 +202,53 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   };
 
-  // Two register buffers: the next tile's item pieces are in flight during this tile's
-  // MFMAs. The loads are inline asm (invisible to the compiler's waits), so every use is
-  // preceded by a hand-counted wait: LT = loads per tile; before computing tile t the only
-  // younger loads allowed in flight are tile t+1's.
+  // Item tiles are prefetched PF tiles ahead into a ring of register buffers. The loads
+  // are inline asm (invisible to the compiler's waits), so every use is preceded by a
+  // hand-counted wait: LT = loads per tile; before computing tile t, only the loads of the
+  // tiles issued after it (at most PF) may still be in flight.
   constexpr int LT = Q / 4;
-  f32x4v afA[LT], afB[LT];
+  auto wait_for = [&](int64_t it) {
+    const int64_t left = (i1 - it - 1) / 16;  // tiles after `it` in this range
+    const int64_t after = left < PF ? left : PF;
+    if (PF >= 2 && after >= 2) wait_vm<2 * LT>();
+    else if (after >= 1) wait_vm<LT>();
+    else wait_vm<0>();
+  };
   __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the prologue loads: vmcnt(0)
-  if (i0 < i1) load_tile(i0, afA);
-  for (int64_t it = i0; it < i1; it += 32) {
-    const bool has_b = it + 16 < i1;
-    if (has_b) {
-      load_tile(it + 16, afB);
-      wait_vm<LT>();
-    } else {
-      wait_vm<0>();
+  if constexpr (PF == 1) {
+    f32x4v afA[LT], afB[LT];
+    if (i0 < i1) load_tile(i0, afA);
+    for (int64_t it = i0; it < i1; it += 32) {
+      if (it + 16 < i1) load_tile(it + 16, afB);
+      wait_for(it);
+      do_tile(it, afA);
+      maybe_compact();
+      if (it + 16 >= i1) break;
+      if (it + 32 < i1) load_tile(it + 32, afA);
+      wait_for(it + 16);
+      do_tile(it + 16, afB);
+      maybe_compact();
     }
-    do_tile(it, afA);
-    if (!has_b) break;
-    if (it + 32 < i1) {
-      load_tile(it + 32, afA);
-      wait_vm<LT>();
-    } else {
-      wait_vm<0>();
+  } else {
+    f32x4v afA[LT], afB[LT], afC[LT];
+    if (i0 < i1) load_tile(i0, afA);
+    if (i0 + 16 < i1) load_tile(i0 + 16, afB);
+    for (int64_t it = i0; it < i1; it += 48) {
+      if (it + 32 < i1) load_tile(it + 32, afC);
+      wait_for(it);
+      do_tile(it, afA);
+      maybe_compact();
+      if (it + 16 >= i1) break;
+      if (it + 48 < i1) load_tile(it + 48, afA);
+      wait_for(it + 16);
+      do_tile(it + 16, afB);
+      maybe_compact();
+      if (it + 32 >= i1) break;
+      if (it + 64 < i1) load_tile(it + 64, afB);
+      wait_for(it + 32);
+      do_tile(it + 32, afC);
+      maybe_compact();
     }
-    do_tile(it + 16, afB);
-    maybe_compact();
   }
   wait_vm<0>();
 
@@ -368,7 +390,7 @@ __global__ __launch_bounds__(256) void k_score_dense(
   }
 }
 
-template <int D, int NG, int M, int WAVES>
+template <int D, int NG, int M, int WAVES, int PF>
 static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
                         const int64_t *ex_rowptr, const int32_t *ex_col, float mask_value,
                         int k, int n_splits, int64_t items_per_split, float *out_val,
@@ -376,10 +398,37 @@ static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64
                         hipStream_t stream) {
   const int64_t users_per_block = (int64_t)WAVES * NG * 16;
   const int64_t tiles = (n_users + users_per_block - 1) / users_per_block;
-  k_score_topk<D, NG, M, WAVES><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
+  k_score_topk<D, NG, M, WAVES, PF><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
                                    stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
                                              mask_value, k, n_splits, items_per_split,
                                              out_val, out_idx, part_val, part_idx);
+}
+
+template <int D, int PF>
+static void dispatch_topk_pf(int M, const float *eu, const float *ei, int64_t n_users,
+                          int64_t n_items, const int64_t *ex_rowptr, const int32_t *ex_col,
+                          float mask_value, int k, int n_splits, int64_t items_per_split,
+                          float *out_val, int64_t *out_idx, float *part_val,
+                          int32_t *part_idx, hipStream_t stream) {
+  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB in every configuration.
+  if (M == 1)
+    launch_topk<D, 2, 1, 4, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else if (M == 2)
+    launch_topk<D, 2, 2, 2, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else
+    launch_topk<D, 1, 4, 2, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+}
+
+// Prefetch depth of the item-tile ring (LGCNHS_TOPK_PF=1|2, read per call; default 2).
+static int topk_pf() {
+  const char *e = getenv("LGCNHS_TOPK_PF");
+  return (e && e[0] == '1') ? 1 : 2;
 }
 
 template <int D>
@@ -388,19 +437,14 @@ static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_use
                           float mask_value, int k, int n_splits, int64_t items_per_split,
                           float *out_val, int64_t *out_idx, float *part_val,
                           int32_t *part_idx, hipStream_t stream) {
-  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB in every configuration.
-  if (M == 1)
-    launch_topk<D, 2, 1, 4>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
-  else if (M == 2)
-    launch_topk<D, 2, 2, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
+  if (topk_pf() == 1)
+    dispatch_topk_pf<D, 1>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                           n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                           stream);
   else
-    launch_topk<D, 1, 4, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
+    dispatch_topk_pf<D, 2>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                           n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                           stream);
 }
 
 static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
