@@ -199,12 +199,15 @@ def as_adjacency(edge_index, n_nodes: int, device=None) -> Adjacency:
         return edge_index
     t = torch.as_tensor(edge_index)
     key = (t.data_ptr(), tuple(t.shape), str(t.device), t._version, int(n_nodes), str(device))
-    adj = _ADJ_CACHE.get(key)
-    if adj is None:
-        if t.numel() and (int(t.min()) < 0 or int(t.max()) >= n_nodes):
-            raise ValueError(f"edge_index has node ids outside [0, {n_nodes})")
-        adj = Adjacency.from_edge_index(t, n_nodes, device=device)
-        if len(_ADJ_CACHE) >= 8:
-            _ADJ_CACHE.pop(next(iter(_ADJ_CACHE)))
-        _ADJ_CACHE[key] = adj
+    hit = _ADJ_CACHE.get(key)
+    # the cache holds a reference to the keyed tensor, so its storage (and data_ptr) can
+    # not be recycled for another tensor while the entry lives
+    if hit is not None and hit[0] is t:
+        return hit[1]
+    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= n_nodes):
+        raise ValueError(f"edge_index has node ids outside [0, {n_nodes})")
+    adj = Adjacency.from_edge_index(t, n_nodes, device=device)
+    if len(_ADJ_CACHE) >= 8:
+        _ADJ_CACHE.pop(next(iter(_ADJ_CACHE)))
+    _ADJ_CACHE[key] = (t, adj)
     return adj
