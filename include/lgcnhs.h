@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 2
+#define LG_ABI_VERSION 3
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -88,6 +88,8 @@ int lg_gcn_edge_weight_f32(const int64_t *rowptr, const int32_t *src, const floa
  * full-size arrays and their own row range). dim in {32, 64, 128, 256}. w (optional) is
  * the per-entry gcn_norm weight of lg_gcn_edge_weight_f32, indexed like src; passing it
  * streams 4 B/edge instead of gathering dis[s]. y must not alias x.
+ * Rows with more than long_threshold entries (<= 0: none) are skipped; the caller runs
+ * them through lg_spmm_long_rows_f32 (power-law hubs).
  * ------------------------------------------------------------------------------------ */
 enum lg_acc_mode {
   LG_ACC_NONE = 0,
@@ -97,9 +99,22 @@ enum lg_acc_mode {
   LG_ACC_ONLY = 4,
 };
 int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
-                      const float *w, const float *x, float *y, const float *x0, float *acc, float *out,
-                      int64_t n_rows, int64_t row_offset, int32_t dim, int32_t acc_mode,
-                      float denom, lg_stream_t stream);
+                      const float *w, const float *x, float *y, const float *x0, float *acc,
+                      float *out, int64_t n_rows, int64_t row_offset, int32_t dim,
+                      int32_t acc_mode, float denom, int64_t long_threshold,
+                      lg_stream_t stream);
+
+/* The long rows skipped above, cut into segments [seg_beg[s], seg_end[s]) of src/w
+ * (seg_node[s] = node id of the segment's row): one wave per segment writes a partial sum
+ * into partial[n_seg, dim] (caller-owned workspace), then long row j (node long_node[j],
+ * segments seg_ptr[j] .. seg_ptr[j+1]) adds its partials in order and runs the same
+ * y / acc_mode epilogue as lg_spmm_layer_f32. Deterministic (no atomics). */
+int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_end,
+                          const int32_t *seg_node, int64_t n_seg, const int32_t *long_node,
+                          const int64_t *seg_ptr, int64_t n_long, const int32_t *src,
+                          const float *dis, const float *w, const float *x, float *y,
+                          const float *x0, float *acc, float *out, int32_t dim,
+                          int32_t acc_mode, float denom, float *partial, lg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Full-catalog scoring with exclusion mask and top-K.

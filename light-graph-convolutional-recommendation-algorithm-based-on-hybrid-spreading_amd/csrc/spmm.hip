@@ -5,7 +5,8 @@
 // msg = norm.view(-1,1) * x_j  (message, :84);  out = zeros.scatter_add_(0, col, msg).
 // Here every destination row is owned by one wave, the nnz x d message tensor never
 // exists, the edge weight dis[s]*dis[g] (gcn_norm) is streamed per entry or recomputed,
-// and the running layer sum of torch.stack(...).mean(1) (:66-69) is fused into the epilogue.
+// and the running layer sum of torch.stack(...).mean(1) (:66-69) is fused into the
+// epilogue.
 //
 // Layout / mapping (HBM-bound gather):
 //   - embedding rows are fp32 [N, D]; a row is D*4 bytes = LPR lanes x 16 B (float4).
@@ -21,6 +22,12 @@
 //     table from the Infinity Cache.
 //   - UNROLL edge slots per group are in flight before the accumulate.
 //   - group partial sums are combined with an xor butterfly; deterministic order.
+//
+// Power-law rows: a row longer than `long_threshold` would serialise on one wave (a
+// 10M-edge hub = 2.4 GB through one wave). The main kernel skips such rows; the caller
+// cuts them into segments, k_spmm_segments gives each segment its own wave (partial sums
+// in a workspace) and k_spmm_long_reduce adds a row's segments in order and runs the same
+// epilogue. Still atomic-free and bitwise reproducible.
 #include "common.h"
 
 namespace lg {
@@ -32,26 +39,27 @@ __device__ __forceinline__ void nt_store4(float *p, const float4 &v) {
   __builtin_nontemporal_store(t, reinterpret_cast<f32x4v *>(p));
 }
 
+__device__ __forceinline__ void add4(float4 &a, const float4 &b) {
+  a.x = __fadd_rn(a.x, b.x);
+  a.y = __fadd_rn(a.y, b.y);
+  a.z = __fadd_rn(a.z, b.z);
+  a.w = __fadd_rn(a.w, b.w);
+}
+
+// sum over entries [beg, end) of w_e * x[src_e] for this lane's float4 slice, combined over
+// the wave's lane groups (every group ends with the full sum).
 template <int D, int UNROLL>
-__global__ __launch_bounds__(256) void k_spmm_layer(
-    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ src,
-    const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
-    float *__restrict__ y,
-    const float *__restrict__ x0, float *acc, float *out, int64_t n_rows,
-    int64_t row_offset, int mode, float denom) {
-  constexpr int LPR = D / 4;   // lanes per embedding row (float4 each)
-  constexpr int G = 64 / LPR;  // rows gathered per wave-instruction
+__device__ __forceinline__ float4 gather_sum(int64_t beg, int64_t end,
+                                             const int32_t *__restrict__ src,
+                                             const float *__restrict__ w,
+                                             const float *__restrict__ dis, float dg,
+                                             const float *__restrict__ x) {
+  constexpr int LPR = D / 4;
+  constexpr int G = 64 / LPR;
   const int lane = lane_id();
   const int gi = lane / LPR;
   const int li = lane % LPR;
-  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  if (r >= n_rows) return;  // wave-uniform
-  const int64_t g = row_offset + r;
-  const int64_t beg = rowptr[r];
-  const int64_t end = rowptr[r + 1];
-  const float dg = dis[g];
   const float4 *__restrict__ x4 = reinterpret_cast<const float4 *>(x);
-
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t cb = beg; cb < end; cb += 64) {
     const int n = (int)((end - cb) < 64 ? (end - cb) : 64);
@@ -97,7 +105,15 @@ __global__ __launch_bounds__(256) void k_spmm_layer(
     sum.z = __fadd_rn(sum.z, __shfl_xor(sum.z, off));
     sum.w = __fadd_rn(sum.w, __shfl_xor(sum.w, off));
   }
-  if (gi != 0) return;
+  return sum;
+}
+
+// y / layer-mean epilogue for node g, float4 slice li (called by lane group 0 only).
+template <int D>
+__device__ __forceinline__ void epilogue(int64_t g, int li, const float4 &sum,
+                                         float *__restrict__ y, const float *__restrict__ x0,
+                                         float *acc, float *out, int mode, float denom) {
+  constexpr int LPR = D / 4;
   const int64_t o = g * LPR + li;
   if (y) nt_store4(y + o * 4, sum);
   float4 a;
@@ -108,10 +124,7 @@ __global__ __launch_bounds__(256) void k_spmm_layer(
     case LG_ACC_LAST: a = reinterpret_cast<const float4 *>(acc)[o]; break;
     default: return;
   }
-  a.x = __fadd_rn(a.x, sum.x);
-  a.y = __fadd_rn(a.y, sum.y);
-  a.z = __fadd_rn(a.z, sum.z);
-  a.w = __fadd_rn(a.w, sum.w);
+  add4(a, sum);
   if (mode == LG_ACC_LAST || mode == LG_ACC_ONLY) {
     a.x = __fdiv_rn(a.x, denom);
     a.y = __fdiv_rn(a.y, denom);
@@ -123,16 +136,101 @@ __global__ __launch_bounds__(256) void k_spmm_layer(
   }
 }
 
+template <int D, int UNROLL>
+__global__ __launch_bounds__(256) void k_spmm_layer(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ src,
+    const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
+    float *__restrict__ y, const float *__restrict__ x0, float *acc, float *out,
+    int64_t n_rows, int64_t row_offset, int mode, float denom, int64_t long_threshold) {
+  constexpr int LPR = D / 4;
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (r >= n_rows) return;  // wave-uniform
+  const int64_t beg = rowptr[r];
+  const int64_t end = rowptr[r + 1];
+  if (end - beg > long_threshold) return;  // done by the segmented path
+  const int64_t g = row_offset + r;
+  const float4 sum = gather_sum<D, UNROLL>(beg, end, src, w, dis, dis[g], x);
+  const int lane = lane_id();
+  if (lane / LPR != 0) return;
+  epilogue<D>(g, lane % LPR, sum, y, x0, acc, out, mode, denom);
+}
+
+// one wave per segment: partial[s] = sum over [seg_beg[s], seg_end[s]) of w_e * x[src_e]
+template <int D, int UNROLL>
+__global__ __launch_bounds__(256) void k_spmm_segments(
+    const int64_t *__restrict__ seg_beg, const int64_t *__restrict__ seg_end,
+    const int32_t *__restrict__ seg_node, const int32_t *__restrict__ src,
+    const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
+    float *__restrict__ partial, int64_t n_seg) {
+  constexpr int LPR = D / 4;
+  const int64_t sgi = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (sgi >= n_seg) return;
+  const float4 sum = gather_sum<D, UNROLL>(seg_beg[sgi], seg_end[sgi], src, w, dis,
+                                           dis[seg_node[sgi]], x);
+  const int lane = lane_id();
+  if (lane / LPR != 0) return;
+  reinterpret_cast<float4 *>(partial)[sgi * LPR + lane % LPR] = sum;
+}
+
+// one wave per long row j: its segments [seg_ptr[j], seg_ptr[j+1]) summed in order.
+template <int D>
+__global__ __launch_bounds__(256) void k_spmm_long_reduce(
+    const int32_t *__restrict__ long_node, const int64_t *__restrict__ seg_ptr,
+    const float *__restrict__ partial, float *__restrict__ y, const float *__restrict__ x0,
+    float *acc, float *out, int64_t n_long, int mode, float denom) {
+  constexpr int LPR = D / 4;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (j >= n_long) return;
+  const int lane = lane_id();
+  if (lane / LPR != 0) return;  // one lane group sums the segments sequentially
+  const int li = lane % LPR;
+  const float4 *p4 = reinterpret_cast<const float4 *>(partial);
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t s = seg_ptr[j]; s < seg_ptr[j + 1]; ++s) add4(sum, p4[s * LPR + li]);
+  epilogue<D>(long_node[j], li, sum, y, x0, acc, out, mode, denom);
+}
+
 template <int D>
 static void launch_spmm(const int64_t *rowptr, const int32_t *src, const float *dis,
-                        const float *w, const float *x, float *y, const float *x0, float *acc, float *out,
-                        int64_t n_rows, int64_t row_offset, int mode, float denom,
-                        hipStream_t stream) {
+                        const float *w, const float *x, float *y, const float *x0, float *acc,
+                        float *out, int64_t n_rows, int64_t row_offset, int mode, float denom,
+                        int64_t long_threshold, hipStream_t stream) {
   constexpr int WPB = 4;  // waves (rows) per 256-thread block
   constexpr int UNROLL = (D <= 64) ? 4 : 8;
   const int64_t blocks = (n_rows + WPB - 1) / WPB;
   k_spmm_layer<D, UNROLL><<<dim3((unsigned)blocks), dim3(64 * WPB), 0, stream>>>(
-      rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom);
+      rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
+      long_threshold);
+}
+
+template <int D>
+static void launch_long(const int64_t *seg_beg, const int64_t *seg_end,
+                        const int32_t *seg_node, int64_t n_seg, const int32_t *long_node,
+                        const int64_t *seg_ptr, int64_t n_long, const int32_t *src,
+                        const float *dis, const float *w, const float *x, float *y,
+                        const float *x0, float *acc, float *out, int mode, float denom,
+                        float *partial, hipStream_t stream) {
+  constexpr int UNROLL = (D <= 64) ? 4 : 8;
+  if (n_seg > 0)
+    k_spmm_segments<D, UNROLL><<<dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, stream>>>(
+        seg_beg, seg_end, seg_node, src, dis, w, x, partial, n_seg);
+  k_spmm_long_reduce<D><<<dim3((unsigned)((n_long + 3) / 4)), dim3(256), 0, stream>>>(
+      long_node, seg_ptr, partial, y, x0, acc, out, n_long, mode, denom);
+}
+
+static int check_modes(int acc_mode, const float *x0, const float *acc, const float *out,
+                       float denom, const float *x, const float *y, const char *fn) {
+  LG_REQUIRE(acc_mode >= LG_ACC_NONE && acc_mode <= LG_ACC_ONLY, "%s: bad acc_mode %d", fn,
+             acc_mode);
+  LG_REQUIRE(!(acc_mode == LG_ACC_FIRST || acc_mode == LG_ACC_ONLY) || x0,
+             "%s: acc_mode needs x0", fn);
+  LG_REQUIRE(!(acc_mode == LG_ACC_FIRST || acc_mode == LG_ACC_MID || acc_mode == LG_ACC_LAST) ||
+                 acc,
+             "%s: acc_mode needs acc", fn);
+  LG_REQUIRE(!(acc_mode == LG_ACC_LAST || acc_mode == LG_ACC_ONLY) || (out && denom != 0.f),
+             "%s: acc_mode needs out and a non-zero denom", fn);
+  LG_REQUIRE(y != x || !y, "%s: y must not alias x (ping-pong the layer buffers)", fn);
+  return LG_OK;
 }
 
 }  // namespace lg
@@ -143,28 +241,48 @@ extern "C" int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src,
                                  const float *dis, const float *w, const float *x, float *y,
                                  const float *x0, float *acc, float *out, int64_t n_rows,
                                  int64_t row_offset, int32_t dim, int32_t acc_mode,
-                                 float denom, lg_stream_t stream) {
+                                 float denom, int64_t long_threshold, lg_stream_t stream) {
   LG_REQUIRE(rowptr && dis && x && n_rows >= 0 && row_offset >= 0,
              "lg_spmm_layer_f32: null pointer or negative size");
   LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
              "lg_spmm_layer_f32: dim %d not in {32,64,128,256}", dim);
-  LG_REQUIRE(acc_mode >= LG_ACC_NONE && acc_mode <= LG_ACC_ONLY,
-             "lg_spmm_layer_f32: bad acc_mode %d", acc_mode);
-  LG_REQUIRE(!(acc_mode == LG_ACC_FIRST || acc_mode == LG_ACC_ONLY) || x0,
-             "lg_spmm_layer_f32: acc_mode needs x0");
-  LG_REQUIRE(!(acc_mode == LG_ACC_FIRST || acc_mode == LG_ACC_MID || acc_mode == LG_ACC_LAST) ||
-                 acc,
-             "lg_spmm_layer_f32: acc_mode needs acc");
-  LG_REQUIRE(!(acc_mode == LG_ACC_LAST || acc_mode == LG_ACC_ONLY) || (out && denom != 0.f),
-             "lg_spmm_layer_f32: acc_mode needs out and a non-zero denom");
-  LG_REQUIRE(y != x, "lg_spmm_layer_f32: y must not alias x (ping-pong the layer buffers)");
+  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, "lg_spmm_layer_f32");
+  if (st != LG_OK) return st;
   if (n_rows == 0) return LG_OK;
+  if (long_threshold <= 0) long_threshold = INT64_MAX;
   hipStream_t s = (hipStream_t)stream;
   switch (dim) {
-    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, s); break;
-    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, s); break;
-    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, s); break;
-    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, s); break;
+    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
+    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
+    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
+    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
   }
   return launch_status("lg_spmm_layer_f32");
+}
+
+extern "C" int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_end,
+                                     const int32_t *seg_node, int64_t n_seg,
+                                     const int32_t *long_node, const int64_t *seg_ptr,
+                                     int64_t n_long, const int32_t *src, const float *dis,
+                                     const float *w, const float *x, float *y,
+                                     const float *x0, float *acc, float *out, int32_t dim,
+                                     int32_t acc_mode, float denom, float *partial,
+                                     lg_stream_t stream) {
+  LG_REQUIRE(n_seg >= 0 && n_long >= 0, "lg_spmm_long_rows_f32: negative size");
+  if (n_long == 0) return LG_OK;
+  LG_REQUIRE(seg_beg && seg_end && seg_node && long_node && seg_ptr && src && dis && x &&
+                 partial,
+             "lg_spmm_long_rows_f32: null pointer");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
+             "lg_spmm_long_rows_f32: dim %d not in {32,64,128,256}", dim);
+  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, "lg_spmm_long_rows_f32");
+  if (st != LG_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dim) {
+    case 32: launch_long<32>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
+    case 64: launch_long<64>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
+    case 128: launch_long<128>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
+    default: launch_long<256>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
+  }
+  return launch_status("lg_spmm_long_rows_f32");
 }

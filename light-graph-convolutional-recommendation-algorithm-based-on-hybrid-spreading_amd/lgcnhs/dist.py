@@ -87,15 +87,17 @@ class RowShard:
 
 
 def hip_layer(shard: RowShard, piece, dis, x, y, x0, acc, out, mode, denom):
-    from . import _native as N
+    from .graph import LONG_ROW_SEGMENT, LONG_ROW_THRESHOLD, LongRowPlan
+    from .ops import run_layer
     lb, le, off = piece
     if le <= lb:
         return
-    w = None if shard.weight is None else shard.weight
-    N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(shard.rowptr[lb:]), N.ptr(shard.src), N.ptr(dis), N.ptr(w), N.ptr(x),
-        N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), le - lb, off, x.shape[1], mode,
-        float(denom), N.stream_handle(x.device)), "lg_spmm_layer_f32")
+    plans = shard.__dict__.setdefault("_plans", {})
+    if piece not in plans:
+        plans[piece] = LongRowPlan(shard.rowptr[lb:le + 1], off, LONG_ROW_THRESHOLD,
+                                   LONG_ROW_SEGMENT)
+    run_layer(shard.rowptr[lb:], shard.src, dis, shard.weight, x, y, x0, acc, out, le - lb,
+              off, mode, denom, plans[piece])
 
 
 def _gather_block(buf: torch.Tensor, shard: RowShard, c: int, group=None, async_op=True):

@@ -38,6 +38,40 @@ def _sorted_unique_keys(rows: torch.Tensor, cols: torch.Tensor, n_cols: int,
     return keys
 
 
+LONG_ROW_THRESHOLD = 4096   # rows with more entries go through the segmented path
+LONG_ROW_SEGMENT = 2048     # entries per segment (one wave each)
+
+
+class LongRowPlan:
+    """Segments of the rows of a CSR slice longer than the threshold (power-law hubs),
+    for lg_spmm_long_rows_f32. Node ids are ``row_offset + local row``."""
+
+    def __init__(self, rowptr: torch.Tensor, row_offset: int, threshold: int, seg_len: int):
+        self.threshold, self.seg_len = int(threshold), int(seg_len)
+        deg = rowptr[1:] - rowptr[:-1]
+        long_r = torch.nonzero(deg > threshold).flatten()
+        self.n_long = int(long_r.numel())
+        dev = rowptr.device
+        if self.n_long == 0:
+            self.n_seg = 0
+            return
+        beg, end = rowptr[long_r], rowptr[long_r + 1]
+        nseg = (end - beg + seg_len - 1) // seg_len
+        self.seg_ptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
+                                  torch.cumsum(nseg, 0)])
+        self.n_seg = int(self.seg_ptr[-1])
+        owner = torch.repeat_interleave(torch.arange(self.n_long, device=dev), nseg)
+        k = torch.arange(self.n_seg, device=dev) - self.seg_ptr[owner]
+        self.seg_beg = beg[owner] + k * seg_len
+        self.seg_end = torch.minimum(self.seg_beg + seg_len, end[owner])
+        nodes = (long_r + row_offset).to(torch.int32)
+        self.long_node = nodes
+        self.seg_node = nodes[owner].contiguous()
+
+    def partial(self, dim: int, device) -> torch.Tensor:
+        return torch.empty((max(self.n_seg, 1), dim), dtype=torch.float32, device=device)
+
+
 class Adjacency:
     """Target-major CSR of a message-passing graph over ``n_nodes`` nodes."""
 
@@ -51,6 +85,7 @@ class Adjacency:
         self._dis = None
         self._transpose = None
         self._edge_weight = None
+        self._long_plan = None
 
     @property
     def device(self):
@@ -114,6 +149,11 @@ class Adjacency:
                                             N.stream_handle(self.device)), "lg_gcn_norm_f32")
             self._dis = dis
         return self._dis
+
+    def long_plan(self) -> LongRowPlan:
+        if self._long_plan is None:
+            self._long_plan = LongRowPlan(self.rowptr, 0, LONG_ROW_THRESHOLD, LONG_ROW_SEGMENT)
+        return self._long_plan
 
     def edge_weight(self) -> torch.Tensor:
         """gcn_norm's per-edge weight in this CSR's entry order."""

@@ -27,19 +27,34 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------ propagation
-def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
-               row_begin: int = 0, row_end: int | None = None,
-               stream_weights: bool = True) -> None:
-    """One lg_spmm_layer_f32 launch over rows [row_begin, row_end) of ``adj``; with
-    stream_weights the precomputed gcn_norm edge weights are streamed (else recomputed
-    from dis; identical values)."""
-    if row_end is None:
-        row_end = adj.n_nodes
-    w = adj.edge_weight() if stream_weights else None
+def run_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows: int, row_offset: int,
+              mode: int, denom: float, plan=None) -> None:
+    """One propagation layer over a CSR slice: lg_spmm_layer_f32 for the ordinary rows and,
+    when the slice has rows above the long-row threshold, lg_spmm_long_rows_f32 for them."""
+    dim = x.shape[1]
+    thr = plan.threshold if (plan is not None and plan.n_long) else 0
+    strm = N.stream_handle(x.device)
     N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(adj.rowptr[row_begin:]), N.ptr(adj.src), N.ptr(adj.dis()), N.ptr(w), N.ptr(x),
-        N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), row_end - row_begin, row_begin,
-        x.shape[1], mode, float(denom), N.stream_handle(x.device)), "lg_spmm_layer_f32")
+        N.ptr(rowptr), N.ptr(src), N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0),
+        N.ptr(acc), N.ptr(out), n_rows, row_offset, dim, mode, float(denom), thr, strm),
+        "lg_spmm_layer_f32")
+    if thr:
+        part = plan.partial(dim, x.device)
+        N.check(N.lib().lg_spmm_long_rows_f32(
+            N.ptr(plan.seg_beg), N.ptr(plan.seg_end), N.ptr(plan.seg_node), plan.n_seg,
+            N.ptr(plan.long_node), N.ptr(plan.seg_ptr), plan.n_long, N.ptr(src), N.ptr(dis),
+            N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), dim, mode,
+            float(denom), N.ptr(part), strm), "lg_spmm_long_rows_f32")
+
+
+def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
+               stream_weights: bool = True, long_rows: bool = True) -> None:
+    """One layer over all rows of ``adj``; with stream_weights the precomputed gcn_norm
+    edge weights are streamed (else recomputed from dis; identical values); with
+    long_rows, hub rows go through the segmented path."""
+    w = adj.edge_weight() if stream_weights else None
+    run_layer(adj.rowptr, adj.src, adj.dis(), w, x, y, x0, acc, out, adj.n_nodes, 0, mode,
+              denom, adj.long_plan() if long_rows else None)
 
 
 def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:

@@ -162,3 +162,29 @@ def test_large_graph_properties():
     lhs = ops.propagate(adj, 2.0 * x + z, 3)
     rhs = 2.0 * ops.propagate(adj, x, 3) + ops.propagate(adj, z, 3)
     assert (lhs - rhs).abs().max().item() < 1e-5
+
+
+def test_power_law_hub_rows_segmented():
+    """Zipf(1.1) items: hub rows above the long-row threshold go through the segmented
+    path; the result matches the oracle and the one-wave-per-row path, and repeats bitwise."""
+    from lgcnhs import ops, _native as N
+    from lgcnhs import graph as G
+    from lgcnhs.graph import Adjacency
+    U, I, E = 60_000, 5_000, 600_000
+    users, items = _synth_graph(U, I, E, seed=9, dist="zipf")
+    adj = Adjacency.from_interactions(torch.as_tensor(users), torch.as_tensor(items), U, I, DEV)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu()
+    assert int(deg.max()) > 4 * G.LONG_ROW_THRESHOLD  # real hubs
+    plan = adj.long_plan()
+    assert plan.n_long > 0 and plan.n_seg > plan.n_long
+    e0 = (torch.randn(U + I, 64, generator=torch.Generator().manual_seed(3)) * 0.1)
+    out = ops.propagate(adj, e0.to(DEV), 2)
+    assert torch.equal(out, ops.propagate(adj, e0.to(DEV), 2))
+    coo = torch.as_tensor(O.coo_adjacency(U, I, users, items))
+    uf, itf = O.lightgcn_forward(coo, e0[:U], e0[U:], 2)
+    np.testing.assert_allclose(out.cpu().numpy(), torch.cat([uf, itf]).numpy(), rtol=0, atol=TOL)
+    x = e0.to(DEV)
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    ops.spmm_layer(adj, x, y1, None, None, None, N.LG_ACC_NONE, 1.0, long_rows=True)
+    ops.spmm_layer(adj, x, y2, None, None, None, N.LG_ACC_NONE, 1.0, long_rows=False)
+    np.testing.assert_allclose(y1.cpu().numpy(), y2.cpu().numpy(), rtol=0, atol=1e-6)

@@ -33,7 +33,7 @@ def test_argument_validation_without_gpu():
     lib = N.load_library()
     z = ctypes.c_void_p(0)
     one = ctypes.c_void_p(16)  # never dereferenced: validation fails first
-    st = lib.lg_spmm_layer_f32(one, one, one, z, one, z, z, z, z, 10, 0, 48, 0, 1.0, z)
+    st = lib.lg_spmm_layer_f32(one, one, one, z, one, z, z, z, z, 10, 0, 48, 0, 1.0, 0, z)
     assert st == 1 and b"dim" in lib.lg_last_error()
     st = lib.lg_score_topk_f32(one, one, 4, 4, 64, z, z, -1024.0, 0, 1, one, one, z, 0, z)
     assert st == 1 and b"k=0" in lib.lg_last_error()
@@ -41,7 +41,7 @@ def test_argument_validation_without_gpu():
     assert st == 1
     st = lib.lg_rows_topk_f64(one, 4, 4, 4, z, z, 0, z, z, 7, 3, one, one, z)
     assert st == 1 and b"excl_mode" in lib.lg_last_error()
-    st = lib.lg_spmm_layer_f32(one, one, one, z, one, one, z, z, z, 5, 0, 64, 3, 4.0, z)
+    st = lib.lg_spmm_layer_f32(one, one, one, z, one, one, z, z, z, 5, 0, 64, 3, 4.0, 0, z)
     assert st == 1  # LAST needs acc/out
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
