@@ -136,6 +136,45 @@ def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
     return elapsed, sum(kernel_ms) / len(kernel_ms) / 1e3
 
 
+def bench_small_config(dev, k):
+    """configs[1] (ML-1M shape: 6040 users x 3706 items, 800,167 train interactions, d=64,
+    L=3) on one GPU: propagation eager and replayed from a captured hipGraph, and the full
+    masked top-k for every user. Kernels of tens of microseconds: launch-bound."""
+    from lgcnhs import ops
+    from lgcnhs.graph import Adjacency, RowSets
+    U, I, E, D, L = WORKLOADS["c2"]
+    rowptr, src, keys = gen_graph(U, I, E, seed=1, dev=dev)
+    users, items = keys // I, keys % I
+    adj = Adjacency.from_interactions(users, items, U, I, dev)
+    e0 = torch.randn(U + I, D, device=dev, generator=torch.Generator(device=dev).manual_seed(7)) * 0.1
+    ops.propagate(adj, e0, L)
+    pg = ops.PropagationGraph(adj, D, L)
+    res = {"users": U, "items": I, "directed_nnz": adj.nnz, "dim": D, "layers": L}
+    for name, fn in (("eager", lambda: ops.propagate(adj, e0, L)), ("graph", lambda: pg.run(e0))):
+        fn()
+        torch.cuda.synchronize()
+        reps = 50
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        res[f"propagation_{name}_edge_layers_per_s"] = adj.nnz * L / dt
+        res[f"forward_{name}_us"] = dt * 1e6
+    excl = RowSets.from_pairs(users, items, U, I, dev)
+    eu, ei = e0[:U].contiguous(), e0[U:].contiguous()
+    ops.score_topk(eu, ei, k, excl)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ops.score_topk(eu, ei, k, excl)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 10
+    res["topk_all_users_ms"] = dt * 1e3
+    res["topk_recs_per_s"] = U / dt
+    return res
+
+
 def load_traffic(workload, world):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -159,6 +198,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
+    ap.add_argument("--no-small", action="store_true",
+                    help="skip the ML-1M-shaped (configs[1]) side measurement at N=1")
     ap.add_argument("--extra-dims", type=int, nargs="*", default=[128],
                     help="also time the same graph at these embedding widths")
     ap.add_argument("--chunks", type=int, default=0,
@@ -262,6 +303,13 @@ def main():
                 "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
                 "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
 
+    small = None
+    if world == 1 and not args.no_small:
+        try:
+            small = bench_small_config(dev, args.k)
+        except Exception as ex:  # an auxiliary measurement never hides the main result
+            log(f"small-config bench failed: {ex!r}")
+
     cpu = None
     if cpu_src is not None:
         try:
@@ -286,6 +334,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "topk": topk,
             "other_dims": extra,
+            "c2_ml1m_shape": small,
             "cpu_baseline": cpu,
             "host": platform.node(),
         }

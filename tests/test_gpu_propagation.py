@@ -188,3 +188,15 @@ def test_power_law_hub_rows_segmented():
     ops.spmm_layer(adj, x, y1, None, None, None, N.LG_ACC_NONE, 1.0, long_rows=True)
     ops.spmm_layer(adj, x, y2, None, None, None, N.LG_ACC_NONE, 1.0, long_rows=False)
     np.testing.assert_allclose(y1.cpu().numpy(), y2.cpu().numpy(), rtol=0, atol=1e-6)
+
+
+def test_captured_graph_replay_matches_eager():
+    from lgcnhs import ops
+    from lgcnhs.graph import Adjacency
+    users, items = _synth_graph(943, 1682, 80000, seed=1)
+    adj = Adjacency.from_interactions(torch.as_tensor(users), torch.as_tensor(items),
+                                      943, 1682, DEV)
+    pg = ops.PropagationGraph(adj, 64, 3)
+    for seed in (0, 1):
+        e0 = torch.randn(943 + 1682, 64, device=DEV, generator=torch.Generator(device=DEV).manual_seed(seed)) * 0.1
+        assert torch.equal(pg.run(e0).clone(), ops.propagate(adj, e0, 3))
