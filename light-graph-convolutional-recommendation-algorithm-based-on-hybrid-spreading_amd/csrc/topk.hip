@@ -115,7 +115,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   // when that alone beats tau), and entries [chk, n) of a list are binary-searched in the
   // user's sorted exclusion row only when the list is compacted. Exact: an excluded item
   // would enter with mask_value, and mask_value > tau admits every item.
-  auto compact_user = [&](int g, int u) {
+  auto compact_user = [&](int g, int u) __attribute__((always_inline)) {
     const int n = __shfl(cnt[g], u);
     const int c0 = __shfl(chk[g], u);
     const int64_t lo = __shfl(ex_lo[g], u);
@@ -142,13 +142,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   };
 
-  auto load_tile = [&](int64_t it, f32x4v(&af)[Q / 4]) {
+  auto load_tile = [&](int64_t it, f32x4v(&af)[Q / 4]) __attribute__((always_inline)) {
     const int64_t item_l = it + ul;
     const int64_t itc = item_l < n_items ? item_l : n_items - 1;
     asm_load_piece<Q>(ei + itc * D + gq * Q, af);
   };
 
-  auto do_tile = [&](int64_t it, const f32x4v(&af)[Q / 4]) {
+  auto do_tile = [&](int64_t it, const f32x4v(&af)[Q / 4]) __attribute__((always_inline)) {
     f32x4 acc[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   };
 
   // compact every user whose list could overflow on the next tile (+16 max per tile)
-  auto maybe_compact = [&]() {
+  auto maybe_compact = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   // hand-counted wait: LT = loads per tile; before computing tile t, only the loads of the
   // tiles issued after it (at most PF) may still be in flight.
   constexpr int LT = Q / 4;
-  auto wait_for = [&](int64_t it) {
+  auto wait_for = [&](int64_t it) __attribute__((always_inline)) {
     const int64_t left = (i1 - it - 1) / 16;  // tiles after `it` in this range
     const int64_t after = left < PF ? left : PF;
     if (PF >= 2 && after >= 2) wait_vm<2 * LT>();

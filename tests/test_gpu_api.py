@@ -16,9 +16,9 @@ def data():
     rating_df, tr, va, te = synth_dataframes(120, 200, 3000, seed=4)
     rng = np.random.default_rng(0)
     uf = pd.DataFrame({"user_id": np.arange(120),
-                       "user_features": [str(list(rng.random(6).round(3))) for _ in range(120)]})
+                       "user_features": [str([float(v) for v in rng.random(6).round(3)]) for _ in range(120)]})
     itf = pd.DataFrame({"item_id": np.arange(200),
-                        "item_features": [list(rng.random(9).round(3)) for _ in range(200)]})
+                        "item_features": [[float(v) for v in rng.random(9).round(3)] for _ in range(200)]})
     return rating_df, tr, va, te, uf, itf
 
 
