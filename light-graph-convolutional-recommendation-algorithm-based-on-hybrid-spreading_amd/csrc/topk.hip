@@ -20,8 +20,6 @@
 // item takes mask_value (-1024) before the sort, which is exactly the reference's masked
 // top-k. Lists are compacted by the wave-wide bitonic sort of common.h. Order: (score
 // desc, item asc). The main loop thus issues no global load but the item tiles.
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace lg {
@@ -43,16 +41,25 @@ __device__ __forceinline__ void load_piece(const float *__restrict__ p, float (&
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-// Item-tile loads hidden from the compiler's wait analysis (cdna_hip_programming.md §5.7
-// item 1): the compiler's loop merge otherwise waits for the prefetch it just issued. The
-// caller waits by hand with wait_vm<N>() = "all but the N youngest vector-memory ops".
-template <int Q>
-__device__ __forceinline__ void asm_load_piece(const float *p, f32x4v (&v)[Q / 4]) {
+// Item-tile loads: buffer_load through a per-tile descriptor whose base is the tile's first
+// row and whose record count is the bytes left in the table (0 past its end), so rows
+// beyond n_items read as 0 and every tile issues the same LT loads with no branch and no
+// per-lane address arithmetic. Inline asm keeps them invisible to the compiler's wait
+// analysis (cdna_hip_programming.md §5.7 item 1); the caller waits by hand with
+// wait_vm<N>() = "all but the N youngest vector-memory ops".
+template <int D>
+__device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items, int64_t it,
+                                               int voff, f32x4v (&v)[D / 16]) {
+  constexpr int TB = 16 * D * 4;  // bytes of one 16-item tile
+  const int64_t rem = (n_items - it) * (D * 4);
+  const int num = rem <= 0 ? 0 : (rem < TB ? (int)rem : TB);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(ei + it * D), 0, num, 0x00020000);
 #pragma unroll
-  for (int t = 0; t < Q / 4; ++t)
-    asm volatile("global_load_dwordx4 %0, %1, off offset:%2"
+  for (int t = 0; t < D / 16; ++t)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3"
                  : "=v"(v[t])
-                 : "v"(p), "i"(t * 16)
+                 : "v"(voff), "s"(r), "i"(t * 16)
                  : "memory");
 }
 
@@ -63,7 +70,16 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // One wave: NG groups of 16 users; the block's waves work independently.
-template <int D, int NG, int M, int WAVES, int PF>
+//
+// Software pipeline (per wave, one 16-item tile per step t):
+//   wait for tile t+1  ->  MFMAs of tile t+1 into acc[(t+1)%2], interleaved with the
+//   one-max-one-compare filter of tile t's scores in acc[t%2]  ->  issue the loads of tile
+//   t+3 into the register buffer tile t+1 just left  ->  (rare) insert tile t's candidates
+//   ->  compact lists that could overflow.
+// The filter's vector instructions fill the MFMA issue gaps (an f32 16x16x4 MFMA holds the
+// SIMD's vector issue for 8 of its 32 cycles), and each tile's loads are in flight for two
+// steps.
+template <int D, int NG, int M, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
     int64_t n_items, const int64_t *__restrict__ ex_rowptr,
@@ -71,9 +87,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
     float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
   constexpr int Q = D / 4;
+  constexpr int LT = Q / 4;  // buffer loads per tile per lane
   constexpr int CAP = 64 * M;
   __shared__ float cs[WAVES][NG][16][CAP];
   __shared__ int ci[WAVES][NG][16][CAP];
+  __shared__ int exs[WAVES][64];
 
   const int wave = threadIdx.x / 64;
   const int lane = lane_id();
@@ -86,10 +104,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   const int64_t i0 = (int64_t)split * items_per_split;
   int64_t i1 = i0 + items_per_split;
   if (i1 > n_items) i1 = n_items;
+  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;  // items of this split
+  const int n_t = (n_valid + 15) / 16;                // tiles of this split
 
   float uf[NG][Q];
   bool uvalid[NG];
-  int64_t ex_lo[NG], ex_hi[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
   int cnt[NG], chk[NG];
   float tau[NG], thr[NG];
 #pragma unroll
@@ -98,10 +118,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     uvalid[g] = u < n_users;
     const int64_t uu = uvalid[g] ? u : n_users - 1;
     load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
-    ex_lo[g] = 0;
+    ex_pos[g] = 0;
     ex_hi[g] = 0;
     if (ex_rowptr && uvalid[g]) {
-      ex_lo[g] = ex_rowptr[u];
+      ex_pos[g] = ex_rowptr[u];
       ex_hi[g] = ex_rowptr[u + 1];
     }
     cnt[g] = 0;
@@ -112,23 +132,42 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   const uint64_t same_user = 0x0001000100010001ull << ul;
 
   // Exclusion is applied lazily: a candidate enters on its raw score (or on the mask value
-  // when that alone beats tau), and entries [chk, n) of a list are binary-searched in the
-  // user's sorted exclusion row only when the list is compacted. Exact: an excluded item
-  // would enter with mask_value, and mask_value > tau admits every item.
-  auto compact_user = [&](int g, int u) __attribute__((always_inline)) {
+  // when that alone beats tau), and the entries [chk, n) added since the user's last
+  // compaction are checked when the list is compacted. Their items all lie in
+  // [previous limit, lim), and ex_pos is the user's first excluded item not yet passed
+  // (>= the previous limit, or the row start: items below i0 are harmless), so the
+  // excluded items to test are one ascending run ex_col[ex_pos ..) read 64 at a time,
+  // coalesced, and binary-searched in LDS. Exact: an excluded item would enter with
+  // mask_value, and mask_value > tau admits every item.
+  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
     const int n = __shfl(cnt[g], u);
     const int c0 = __shfl(chk[g], u);
-    const int64_t lo = __shfl(ex_lo[g], u);
+    int64_t pos = __shfl(ex_pos[g], u);
     const int64_t hi = __shfl(ex_hi[g], u);
     float *ks = &cs[wave][g][u][0];
     int *is = &ci[wave][g][u][0];
-    if (lo < hi) {
-      for (int e = c0 + lane; e < n; e += 64) {
-        const int32_t item = is[e];
-        const int64_t p = lower_bound_i32(ex_col, lo, hi, item);
-        if (p < hi && ex_col[p] == item) ks[e] = mask_value;
+    if (n > c0) {
+      while (pos < hi) {
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        const int nin = __popcll(__ballot(x < lim));  // ascending: a prefix of the lanes
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        for (int j = c0 + lane; j < n; j += 64) {
+          const int item = is[j];
+          int a = 0, b = nin;  // first index with exs[] >= item
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) ks[j] = mask_value;
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
       }
-      wave_sync();
     }
     float t;
     int tid;
@@ -137,19 +176,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       cnt[g] = nc;
       chk[g] = nc;
       tau[g] = t;
+      ex_pos[g] = pos;
       // a masked (excluded) item would enter with mask_value: admit everything then
       thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
     }
   };
 
-  auto load_tile = [&](int64_t it, f32x4v(&af)[Q / 4]) __attribute__((always_inline)) {
-    const int64_t item_l = it + ul;
-    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
-    asm_load_piece<Q>(ei + itc * D + gq * Q, af);
-  };
-
-  auto do_tile = [&](int64_t it, const f32x4v(&af)[Q / 4]) __attribute__((always_inline)) {
-    f32x4 acc[NG];
+  // acc[g][r] = score(user ubase + 16g + ul, item i0 + 16t + 4gq + r)
+  auto mfma_tile = [&](const f32x4v(&af)[LT], f32x4 (&acc)[NG]) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     // s outer / g inner: NG independent accumulation chains interleave on the MFMA pipe
@@ -159,26 +193,37 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       for (int g = 0; g < NG; ++g)
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s / 4][s % 4], uf[g][s], acc[g], 0,
                                                       0, 0);
+  };
 
-    // acc[g][r] = score(user ubase + 16g + ul, item it + 4*gq + r). Fast path: one max
-    // and one compare per group against thr = the entry threshold (tau, or -inf while the
-    // mask value itself would enter, +inf for padding users); the exact per-score test
-    // runs only when some lane of the wave has a candidate.
+  // Fast filter: one max and one compare per group against thr = the entry threshold (tau,
+  // or -inf while the mask value itself would enter, +inf for padding users).
+  auto any_cand = [&](const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const float m = fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
+      any |= m > thr[g];
+    }
+    return __ballot(any) != 0;
+  };
+
+  // Slow path, taken when some lane of the wave has a candidate in tile t.
+  auto insert_tile = [&](int t, const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
+    const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const float m = fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
       if (__ballot(m > thr[g]) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t item = it + gq * 4 + r;
         const float sc = acc[g][r];
-        const bool cand = item < i1 && sc > thr[g];
+        const bool cand = rel + r < n_valid && sc > thr[g];
         const uint64_t bal = __ballot(cand);
         if (bal) {
           const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
           if (cand) {
             cs[wave][g][ul][pos] = sc;
-            ci[wave][g][ul][pos] = (int)item;
+            ci[wave][g][ul][pos] = (int)i0 + rel + r;
           }
           cnt[g] += __popcll(bal & same_user);
         }
@@ -187,7 +232,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   };
 
   // compact every user whose list could overflow on the next tile (+16 max per tile)
-  auto maybe_compact = [&]() __attribute__((always_inline)) {
+  auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
@@ -196,58 +241,46 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
         while (need) {
           const int u = __ffsll((long long)need) - 1;
           need &= need - 1;
-          compact_user(g, u);
+          compact_user(g, u, lim);
         }
       }
     }
   };
 
-  // Item tiles are prefetched PF tiles ahead into a ring of register buffers. The loads
-  // are inline asm (invisible to the compiler's waits), so every use is preceded by a
-  // hand-counted wait: LT = loads per tile; before computing tile t, only the loads of the
-  // tiles issued after it (at most PF) may still be in flight.
-  constexpr int LT = Q / 4;
-  auto wait_for = [&](int64_t it) __attribute__((always_inline)) {
-    const int64_t left = (i1 - it - 1) / 16;  // tiles after `it` in this range
-    const int64_t after = left < PF ? left : PF;
-    if (PF >= 2 && after >= 2) wait_vm<2 * LT>();
-    else if (after >= 1) wait_vm<LT>();
-    else wait_vm<0>();
+  const int voff = (ul * D + gq * Q) * 4;
+  const int lim_end = (int)i1;
+  auto step_lim = [&](int t) __attribute__((always_inline)) {
+    const int l = (int)i0 + (t + 1) * 16;
+    return l < lim_end ? l : lim_end;
   };
   __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the prologue loads: vmcnt(0)
-  if constexpr (PF == 1) {
+  if (n_t > 0) {
     f32x4v afA[LT], afB[LT];
-    if (i0 < i1) load_tile(i0, afA);
-    for (int64_t it = i0; it < i1; it += 32) {
-      if (it + 16 < i1) load_tile(it + 16, afB);
-      wait_for(it);
-      do_tile(it, afA);
-      maybe_compact();
-      if (it + 16 >= i1) break;
-      if (it + 32 < i1) load_tile(it + 32, afA);
-      wait_for(it + 16);
-      do_tile(it + 16, afB);
-      maybe_compact();
-    }
-  } else {
-    f32x4v afA[LT], afB[LT], afC[LT];
-    if (i0 < i1) load_tile(i0, afA);
-    if (i0 + 16 < i1) load_tile(i0 + 16, afB);
-    for (int64_t it = i0; it < i1; it += 48) {
-      if (it + 32 < i1) load_tile(it + 32, afC);
-      wait_for(it);
-      do_tile(it, afA);
-      maybe_compact();
-      if (it + 16 >= i1) break;
-      if (it + 48 < i1) load_tile(it + 48, afA);
-      wait_for(it + 16);
-      do_tile(it + 16, afB);
-      maybe_compact();
-      if (it + 32 >= i1) break;
-      if (it + 64 < i1) load_tile(it + 64, afB);
-      wait_for(it + 32);
-      do_tile(it + 32, afC);
-      maybe_compact();
+    f32x4 accA[NG], accB[NG];
+    load_item_tile<D>(ei, n_items, i0, voff, afA);
+    load_item_tile<D>(ei, n_items, i0 + 16, voff, afB);
+    wait_vm<LT>();
+    mfma_tile(afA, accA);
+    load_item_tile<D>(ei, n_items, i0 + 32, voff, afA);
+    // invariant at step t: acc[t%2] = tile t; buffer (t+1)%2 = tile t+1 (landed or in
+    // flight); buffer t%2 = tile t+2 in flight
+    for (int t = 0;; t += 2) {
+      // ---- even step: tile t in accA, tile t+1 in afB
+      wait_vm<LT>();
+      mfma_tile(afB, accB);
+      bool hit = any_cand(accA);
+      load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 3) * 16, voff, afB);
+      if (hit) insert_tile(t, accA);
+      maybe_compact(step_lim(t));
+      if (t + 1 >= n_t) break;
+      // ---- odd step: tile t+1 in accB, tile t+2 in afA
+      wait_vm<LT>();
+      mfma_tile(afA, accA);
+      hit = any_cand(accB);
+      load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 4) * 16, voff, afA);
+      if (hit) insert_tile(t + 1, accB);
+      maybe_compact(step_lim(t + 1));
+      if (t + 2 >= n_t) break;
     }
   }
   wait_vm<0>();
@@ -259,7 +292,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     for (int u = 0; u < 16; ++u) {
       const int64_t user = ubase + g * 16 + u;
       if (user >= n_users) break;
-      compact_user(g, u);
+      compact_user(g, u, lim_end);
       const int nc = __shfl(cnt[g], u);
       for (int e = lane; e < k; e += 64) {
         const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
@@ -277,7 +310,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   }
 }
-
 // Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
 template <int M>
 __global__ __launch_bounds__(256) void k_topk_merge(const float *__restrict__ part_val,
@@ -390,7 +422,7 @@ __global__ __launch_bounds__(256) void k_score_dense(
   }
 }
 
-template <int D, int NG, int M, int WAVES, int PF>
+template <int D, int NG, int M, int WAVES>
 static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
                         const int64_t *ex_rowptr, const int32_t *ex_col, float mask_value,
                         int k, int n_splits, int64_t items_per_split, float *out_val,
@@ -398,37 +430,10 @@ static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64
                         hipStream_t stream) {
   const int64_t users_per_block = (int64_t)WAVES * NG * 16;
   const int64_t tiles = (n_users + users_per_block - 1) / users_per_block;
-  k_score_topk<D, NG, M, WAVES, PF><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
-                                   stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
-                                             mask_value, k, n_splits, items_per_split,
-                                             out_val, out_idx, part_val, part_idx);
-}
-
-template <int D, int PF>
-static void dispatch_topk_pf(int M, const float *eu, const float *ei, int64_t n_users,
-                          int64_t n_items, const int64_t *ex_rowptr, const int32_t *ex_col,
-                          float mask_value, int k, int n_splits, int64_t items_per_split,
-                          float *out_val, int64_t *out_idx, float *part_val,
-                          int32_t *part_idx, hipStream_t stream) {
-  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB in every configuration.
-  if (M == 1)
-    launch_topk<D, 2, 1, 4, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
-  else if (M == 2)
-    launch_topk<D, 2, 2, 2, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
-  else
-    launch_topk<D, 1, 4, 2, PF>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                            stream);
-}
-
-// Prefetch depth of the item-tile ring (LGCNHS_TOPK_PF=1|2, read per call; default 2).
-static int topk_pf() {
-  const char *e = getenv("LGCNHS_TOPK_PF");
-  return (e && e[0] == '1') ? 1 : 2;
+  k_score_topk<D, NG, M, WAVES><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
+                                  stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
+                                            mask_value, k, n_splits, items_per_split,
+                                            out_val, out_idx, part_val, part_idx);
 }
 
 template <int D>
@@ -437,14 +442,20 @@ static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_use
                           float mask_value, int k, int n_splits, int64_t items_per_split,
                           float *out_val, int64_t *out_idx, float *part_val,
                           int32_t *part_idx, hipStream_t stream) {
-  if (topk_pf() == 1)
-    dispatch_topk_pf<D, 1>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                           n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                           stream);
+  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB (+256 B per wave) in every
+  // configuration: two blocks per CU.
+  if (M == 1)
+    launch_topk<D, 2, 1, 4>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else if (M == 2)
+    launch_topk<D, 2, 2, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
   else
-    dispatch_topk_pf<D, 2>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
-                           n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
-                           stream);
+    launch_topk<D, 1, 4, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
 }
 
 static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
