@@ -20,6 +20,8 @@
 // item takes mask_value (-1024) before the sort, which is exactly the reference's masked
 // top-k. Lists are compacted by the wave-wide bitonic sort of common.h. Order: (score
 // desc, item asc). The main loop thus issues no global load but the item tiles.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace lg {
@@ -51,8 +53,8 @@ template <int D>
 __device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items, int64_t it,
                                                int voff, f32x4v (&v)[D / 16]) {
   constexpr int TB = 16 * D * 4;  // bytes of one 16-item tile
-  const int64_t rem = (n_items - it) * (D * 4);
-  const int num = rem <= 0 ? 0 : (rem < TB ? (int)rem : TB);
+  const int rem = (int)(n_items - it);  // items left in the table (n_items < 2^31)
+  const int num = rem >= 16 ? TB : (rem > 0 ? rem * (D * 4) : 0);
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc((void *)(ei + it * D), 0, num, 0x00020000);
 #pragma unroll
@@ -61,6 +63,15 @@ __device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items,
                  : "=v"(v[t])
                  : "v"(voff), "s"(r), "i"(t * 16)
                  : "memory");
+}
+
+// max of the four scores of an MFMA result (plain v_max3/v_max: the NaN-quieting
+// canonicalisation fmaxf would add is irrelevant for a threshold test)
+__device__ __forceinline__ float max4(f32x4 a) {
+  float m;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a[0]), "v"(a[1]), "v"(a[2]));
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(m), "v"(a[3]));
+  return m;
 }
 
 template <int N>
@@ -85,7 +96,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     int64_t n_items, const int64_t *__restrict__ ex_rowptr,
     const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
-    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx, int probe) {
   constexpr int Q = D / 4;
   constexpr int LT = Q / 4;  // buffer loads per tile per lane
   constexpr int CAP = 64 * M;
@@ -127,7 +138,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     cnt[g] = 0;
     chk[g] = 0;
     tau[g] = neg_inf<float>();
-    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
+    thr[g] = (uvalid[g] && probe != 1) ? neg_inf<float>() : __builtin_huge_valf();
+    // probe == 1 (measurement builds only, see topk_probe()): no candidate ever enters
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
 
@@ -200,10 +212,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   auto any_cand = [&](const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
     bool any = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const float m = fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
-      any |= m > thr[g];
-    }
+    for (int g = 0; g < NG; ++g) any |= max4(acc[g]) > thr[g];
     return __ballot(any) != 0;
   };
 
@@ -212,8 +221,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const float m = fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
-      if (__ballot(m > thr[g]) == 0) continue;
+      if (__ballot(max4(acc[g]) > thr[g]) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float sc = acc[g][r];
@@ -233,6 +241,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
 
   // compact every user whose list could overflow on the next tile (+16 max per tile)
   auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    if (__ballot(over) == 0) return;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
@@ -422,6 +434,18 @@ __global__ __launch_bounds__(256) void k_score_dense(
   }
 }
 
+// Measurement knob, compiled in only with -DLG_TOPK_PROBE (make EXTRA=-DLG_TOPK_PROBE):
+// LGCNHS_TOPK_PROBE=1 times the scoring loop with no candidate insertion, =2 drops the
+// exclusion sets. Results are wrong under a probe; the product build always passes 0.
+#ifdef LG_TOPK_PROBE
+static int topk_probe() {
+  const char *e = getenv("LGCNHS_TOPK_PROBE");
+  return e ? atoi(e) : 0;
+}
+#else
+static int topk_probe() { return 0; }
+#endif
+
 template <int D, int NG, int M, int WAVES>
 static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
                         const int64_t *ex_rowptr, const int32_t *ex_col, float mask_value,
@@ -433,7 +457,8 @@ static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64
   k_score_topk<D, NG, M, WAVES><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
                                   stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
                                             mask_value, k, n_splits, items_per_split,
-                                            out_val, out_idx, part_val, part_idx);
+                                            out_val, out_idx, part_val, part_idx,
+                                            topk_probe());
 }
 
 template <int D>
@@ -507,6 +532,7 @@ extern "C" int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_use
   }
   hipStream_t s = (hipStream_t)stream;
   const int M = cap_m(k);
+  if (topk_probe() == 2) ex_rowptr = nullptr, ex_col = nullptr;
   switch (dim) {
     case 32: dispatch_topk<32>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
     case 64: dispatch_topk<64>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
