@@ -23,22 +23,44 @@ def kernel_key(name):
 
 
 def main(out_dir, tag, workload="c5-d64", world=1):
+    """Per kernel, the launch shape (grid size) with the most total time is the headline
+    launch (the bench also runs side configurations); every statistic below is over the
+    dispatches of that shape only."""
     g = os.path.join(REPO, "gpurun_out")
-    stats = {}
-    for r in csv.DictReader(open(os.path.join(g, "prof_trace", "run_kernel_stats.csv"))):
-        k = kernel_key(r["Name"])
+    groups = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(g, "prof_trace", "run_kernel_trace.csv"))):
+        k = kernel_key(r["Kernel_Name"])
         if k:
-            stats[k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
-                        "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
+            groups[(k, int(r["Grid_Size_X"]))].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    head = {}
+    for (k, grid), d in groups.items():
+        if k not in head or sum(d) > sum(groups[(k, head[k])]):
+            head[k] = grid
+    stats = {}
+    for k, grid in head.items():
+        d = sorted(groups[(k, grid)])
+        stats[k] = {"grid_size": grid, "calls": len(d), "avg_ms": sum(d) / len(d),
+                    "min_ms": d[0], "max_ms": d[-1]}
     ctr = defaultdict(list)
-    for sub in ("prof_fetch", "prof_write"):
-        for r in csv.DictReader(open(os.path.join(g, sub, "run_counter_collection.csv"))):
+    for sub in ("prof_fetch", "prof_write", "prof_sq"):
+        path = os.path.join(g, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
             k = kernel_key(r["Kernel_Name"])
-            if k:
+            if k and k in head and int(r["Grid_Size"]) == head[k]:
                 ctr[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
     for (k, c), v in ctr.items():
-        stats.setdefault(k, {})[c + "_KiB_per_launch"] = sum(v) / len(v)
+        unit = "_KiB_per_launch" if c.endswith("_SIZE") else "_per_launch"
+        stats[k][c + unit] = sum(v) / len(v)
     for k, s in stats.items():
+        # SQ_VALU_MFMA_BUSY_CYCLES = 32 cycles x MFMAs summed over all 1024 SIMDs;
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, SQ counters)
+        busy, active = s.get("SQ_VALU_MFMA_BUSY_CYCLES_per_launch"), s.get("GRBM_GUI_ACTIVE_per_launch")
+        if busy and active:
+            s["mfma_busy_frac"] = busy / (1024 * active / 8)
+            s["clock_ghz_profiled"] = active / 8 / (s["avg_ms"] * 1e6)
         if "FETCH_SIZE_KiB_per_launch" in s and "WRITE_SIZE_KiB_per_launch" in s:
             s["hbm_bytes_per_launch"] = (2 * s["FETCH_SIZE_KiB_per_launch"]
                                          + s["WRITE_SIZE_KiB_per_launch"]) * 1024
