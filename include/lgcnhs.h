@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 3
+#define LG_ABI_VERSION 4
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -186,6 +186,78 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
                      const float *eu, const float *ei, int32_t dim,
                      const int64_t *ex_rowptr, const int32_t *ex_col, int32_t excl_mode,
                      int32_t k, double *out_val, int64_t *out_idx, lg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Factored spreading over item tiles: the path for catalogs whose I x I general_W / W do
+ * not fit (SURVEY.md §8 a9 "K3s"; C5 = 1M x 1M would need 8 TB per matrix). Same values,
+ * bit for bit, as lg_spread_general_f64 -> lg_hybrid_weight_f64 -> lg_spread_resource_f64
+ * (-> lg_rows_topk_f64), i.e. the reference's getSpreadingGeneralMat / HybridS /
+ * getResource / recommendForAllUser (model/SpreadMethod/model.py:14-99,
+ * model/SpreadMethod/recommend.py:31-50, model/SpreadLightGCN/model.py:151), without ever
+ * holding an I x I or U x I matrix. For each tile [j0, j0 + tile) of item columns the
+ * caller runs: lg_spread_tile_cursor -> lg_spread_tile_bound -> (exclusive prefix of the
+ * bounds = wt_ptr) -> lg_spread_tile_weight_f64 -> lg_spread_tile_resource_f64 per block
+ * of users -> lg_tile_topk_f64. The orchestration (lgcnhs.ops.spread_topk_tiled) is host
+ * code; see DESIGN.md §5 K3s.
+ * ------------------------------------------------------------------------------------ */
+
+/* alpha[i] = k_item[i]^(1 - lambda), beta[i] = k_item[i]^lambda: the HybridS degree
+ * factors (model/SpreadMethod/model.py:74-79), computed with the same pow() as
+ * lg_hybrid_weight_f64. */
+int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
+                          double *alpha, double *beta, lg_stream_t stream);
+
+/* end[v] = first position p >= cur[v] of user v's item row (user_rowptr/user_items, items
+ * ascending) with user_items[p] >= item_end (or the row end). With cur = the row starts
+ * (first tile) or the previous tile's end, user_items[cur[v] .. end[v]) are v's items in
+ * the tile. cur and end must not alias. */
+int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
+                          int64_t n_users, int32_t item_end, const int64_t *cur,
+                          int64_t *end, lg_stream_t stream);
+
+/* bound[i] = sum over users v of item i (item_rowptr/item_users) of end[v] - cur[v]:
+ * the number of (user, tile item) pairs behind W's row i in the tile, an upper bound on the
+ * row's entries. */
+int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
+                         int64_t n_items, const int64_t *cur, const int64_t *end,
+                         int64_t *bound, lg_stream_t stream);
+
+/* Row i of W restricted to the tile, for every item i:
+ *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} fl(1 / k_v))
+ *             / (alpha[i] * beta[j])          (den == 0 -> 1)
+ * written at wt_col/wt_val[wt_ptr[i] .. wt_ptr[i] + wt_len[i]) in ascending j, where
+ * wt_ptr[n_items + 1] is the exclusive prefix of lg_spread_tile_bound's bounds (row
+ * capacities). ws: lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in
+ * [1, 8192]; every item of the tile must lie in [item_begin, item_begin + tile). */
+size_t lg_spread_tile_weight_ws_bytes(int64_t n_items);
+int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                              const int64_t *user_rowptr, const int32_t *user_items,
+                              int64_t n_items, const int64_t *cur, const int64_t *end,
+                              const double *alpha, const double *beta, int32_t item_begin,
+                              int32_t tile, const int64_t *wt_ptr, int32_t *wt_col,
+                              double *wt_val, int32_t *wt_len, void *ws, size_t ws_bytes,
+                              lg_stream_t stream);
+
+/* F[u][j - item_begin] = sum_{i in items(u), ascending} W[i][j] for the n_users rows of
+ * user_rowptr (pass user_rowptr + u0 for a block) and j in [item_begin, item_begin + tile);
+ * F row-major with leading dim ldf >= tile. */
+int lg_spread_tile_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
+                                int64_t n_users, const int64_t *wt_ptr,
+                                const int32_t *wt_len, const int32_t *wt_col,
+                                const double *wt_val, int32_t item_begin, int32_t tile,
+                                double *F, int64_t ldf, lg_stream_t stream);
+
+/* Merge columns [item_begin, item_begin + n_cols) of (G *) F (F[r][0..n_cols), leading dim
+ * ldf; G as in lg_rows_topk_f64 with eu = the rows' user embeddings and ei = all item
+ * embeddings) into running top-K lists io_val/io_idx [n_rows][k] (sorted by value desc,
+ * index asc; index -1 = empty). first != 0 ignores their contents. Exclusions as in
+ * lg_rows_topk_f64 (ex_rowptr indexed by r). Applied over all tiles in ascending order the
+ * lists equal lg_rows_topk_f64 over the full rows. k in [1, 128]. */
+int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int32_t item_begin,
+                     int32_t n_cols, const float *eu, const float *ei, int32_t dim,
+                     const int64_t *ex_rowptr, const int32_t *ex_col, int32_t excl_mode,
+                     int32_t k, int32_t first, double *io_val, int64_t *io_idx,
+                     lg_stream_t stream);
 
 #ifdef __cplusplus
 }

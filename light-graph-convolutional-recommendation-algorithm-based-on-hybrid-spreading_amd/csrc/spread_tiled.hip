@@ -1,0 +1,675 @@
+// K3s: factored hybrid spreading for catalogs whose I x I matrices do not fit (SURVEY.md §8
+// a9 "K3s", C5: 1M x 1M, 100M interactions -> general_W and W would be 8 TB each).
+//
+// Reference (dense numpy fp64, model/SpreadMethod/model.py):
+//   general_W = (A.T / k_u) @ A            :14-27
+//   W = general_W / (k_i^(1-l) (x) k_j^l)   :63-85   (den == 0 -> 1)
+//   F = A @ W                               :88-99
+//   F_new = G * F; per user argsort desc, drop train|val, [:k]
+//                       model/SpreadLightGCN/model.py:151, recommend.py:18-52
+//
+// The items are processed in column tiles [j0, j0 + T). Per tile:
+//   cursor   end[v] = first position of user v's (ascending) item row with item >= j0 + T;
+//            cur[v] (the previous tile's end) marks the first item >= j0, so
+//            items(v) inside the tile = user_items[cur[v] .. end[v])
+//   bound    bound[i] = sum_{v in users(i)} (end[v] - cur[v]) >= entries of W's row i in
+//            the tile; the caller's exclusive prefix of it is wt_ptr (row capacities)
+//   weight   row i of W restricted to the tile: the (item j, user v) pairs of all
+//            v in users(i) sorted by (j, v) in one wave (bitonic, <= 256 pairs), each run
+//            of equal j summed in ascending v, divided by alpha[i] * beta[j]. Rows with
+//            more than 256 pairs (hub items) go through a block-wide dense LDS tile with
+//            the users walked in ascending order. Either way the value is, bit for bit,
+//            lg_spread_general_f64's sum (ascending v, fl(1/k_v)) / lg_hybrid_weight_f64's
+//            den, so the tiled path equals the dense one exactly.
+//   resource F[u][j - j0] = sum_{i in items(u), ascending} W[i][j]: one wave per user, the
+//            tile's accumulator in LDS; row i's entries are distinct columns, so rows are
+//            added one after another without atomics (lg_spread_resource_f64's order).
+//   topk     the tile's columns of (G *) F merged into running per-user top-K lists
+//            (G = e0 score by f32 MFMA, the chain of lg_score_topk_f32, promoted to fp64).
+// Work: the weight pass costs sum_i deg(i) lookups + the 2-hop pairs once per tile (not per
+// user); the resource pass reads deg(u) short row segments per user and tile.
+#include "common.h"
+
+namespace lg {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
+                                                        int64_t n, double lambda,
+                                                        double *__restrict__ alpha,
+                                                        double *__restrict__ beta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // the same pow() calls as k_hybrid_weight (spread.hip)
+  alpha[i] = pow(k_item[i], 1.0 - lambda);
+  beta[i] = pow(k_item[i], lambda);
+}
+
+__global__ __launch_bounds__(256) void k_tile_cursor(const int64_t *__restrict__ user_rowptr,
+                                                     const int32_t *__restrict__ user_items,
+                                                     int64_t n_users, int32_t item_end,
+                                                     const int64_t *__restrict__ cur,
+                                                     int64_t *__restrict__ end) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_users) return;
+  int64_t p = cur[v];
+  const int64_t pe = user_rowptr[v + 1];
+  while (p < pe && user_items[p] < item_end) ++p;
+  end[v] = p;
+}
+
+// one wave per item row
+__global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ item_rowptr,
+                                                    const int32_t *__restrict__ item_users,
+                                                    int64_t n_items,
+                                                    const int64_t *__restrict__ cur,
+                                                    const int64_t *__restrict__ end,
+                                                    int64_t *__restrict__ bound) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (i >= n_items) return;
+  const int lane = lane_id();
+  int64_t s = 0;
+  for (int64_t e = item_rowptr[i] + lane; e < item_rowptr[i + 1]; e += 64) {
+    const int32_t v = item_users[e];
+    s += end[v] - cur[v];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) bound[i] = s;
+}
+
+constexpr int kSortMax = 256;  // pairs per row handled by the in-wave sort
+
+// Sort the n (<= 64*M) staged pairs (key = -item, id = user) of this wave, then reduce runs
+// of equal items in ascending user order and write the row.
+template <int M>
+__device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, int n, int64_t wbase,
+                                               const int64_t *__restrict__ user_rowptr,
+                                               double alpha_i, const double *__restrict__ beta,
+                                               int32_t *__restrict__ wt_col,
+                                               double *__restrict__ wt_val) {
+  const int lane = lane_id();
+  int k[M], id[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const int e = j * 64 + lane;
+    if (e < n) { k[j] = skey[e]; id[j] = sid[e]; }
+    else { k[j] = INT32_MIN; id[j] = kPadId; }
+  }
+  wave_sync();
+  // before(): key desc, id asc  ->  item asc, user asc; padding (INT32_MIN) last
+  wave_bitonic_sort<int, M>(k, id);
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const int e = j * 64 + lane;
+    skey[e] = k[j];
+    sid[e] = id[j];
+  }
+  wave_sync();
+  int base = 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const int e = j * 64 + lane;
+    const bool head = e < n && (e == 0 || skey[e] != skey[e - 1]);
+    const uint64_t hb = __ballot(head);
+    if (head) {
+      // run e, e+1, ... of one item, users ascending: 0.0 + w0 + w1 + ... in that order
+      const int item = -skey[e];
+      double s = 0.0;
+      for (int m = e; m < n && skey[m] == skey[e]; ++m) {
+        const int32_t v = sid[m];
+        s += 1.0 / (double)(user_rowptr[v + 1] - user_rowptr[v]);
+      }
+      double den = alpha_i * beta[item];
+      if (den == 0.0) den = 1.0;
+      const int pos = base + __popcll(hb & lanemask_lt());
+      wt_col[wbase + pos] = item;
+      wt_val[wbase + pos] = s / den;
+    }
+    base += __popcll(hb);
+  }
+  return base;
+}
+
+// one wave per item row; LDS staging of kSortMax pairs per wave
+__global__ __launch_bounds__(256) void k_tile_weight(
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_items, const int64_t *__restrict__ cur, const int64_t *__restrict__ end,
+    const double *__restrict__ alpha, const double *__restrict__ beta,
+    const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
+    double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
+  __shared__ int skey[4][kSortMax];
+  __shared__ int sid[4][kSortMax];
+  const int wave = threadIdx.x / 64;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  if (i >= n_items) return;
+  const int lane = lane_id();
+  const int64_t wbase = wt_ptr[i];
+  const int64_t bound = wt_ptr[i + 1] - wbase;
+  if (bound == 0) {
+    if (lane == 0) wt_len[i] = 0;
+    return;
+  }
+  if (bound > kSortMax) return;  // hub row: k_tile_weight_hub
+  // stage the pairs: users of i in ascending order, each user's items inside the tile
+  int n = 0;
+  for (int64_t e0 = item_rowptr[i]; e0 < item_rowptr[i + 1]; e0 += 64) {
+    const int64_t e = e0 + lane;
+    int32_t v = 0;
+    int64_t s = 0, t = 0;
+    if (e < item_rowptr[i + 1]) {
+      v = item_users[e];
+      s = cur[v];
+      t = end[v];
+    }
+    const int c = (int)(t - s);
+    // exclusive prefix of c over the lanes
+    int pre = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(pre, o);
+      if (lane >= o) pre += y;
+    }
+    const int total = __shfl(pre, 63);
+    pre -= c;
+    for (int q = 0; q < c; ++q) {
+      skey[wave][n + pre + q] = -user_items[s + q];
+      sid[wave][n + pre + q] = v;
+    }
+    n += total;
+  }
+  wave_sync();
+  int len;
+  if (n <= 64)
+    len = sort_reduce_row<1>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+                             wt_col, wt_val);
+  else if (n <= 128)
+    len = sort_reduce_row<2>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+                             wt_col, wt_val);
+  else
+    len = sort_reduce_row<4>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+                             wt_col, wt_val);
+  if (lane == 0) wt_len[i] = len;
+}
+
+// Hub rows (> kSortMax pairs): one 256-thread block per row (grid-stride over the hub list),
+// the tile as a dense LDS accumulator, users walked in ascending order as in
+// k_spread_general.
+__global__ __launch_bounds__(256) void k_tile_weight_hub(
+    const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    const int64_t *__restrict__ cur, const int64_t *__restrict__ end,
+    const double *__restrict__ alpha, const double *__restrict__ beta, int32_t item_begin,
+    int32_t tile, const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
+    double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
+  extern __shared__ double acc[];  // tile doubles
+  __shared__ int wsum[4];
+  const int64_t nh = *n_hub;
+  for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int64_t i = hub_rows[h];
+    for (int j = threadIdx.x; j < tile; j += blockDim.x) acc[j] = 0.0;
+    __syncthreads();
+    for (int64_t e = item_rowptr[i]; e < item_rowptr[i + 1]; ++e) {
+      const int32_t v = item_users[e];
+      const double wv = 1.0 / (double)(user_rowptr[v + 1] - user_rowptr[v]);
+      for (int64_t p = cur[v] + threadIdx.x; p < end[v]; p += blockDim.x)
+        acc[user_items[p] - item_begin] += wv;
+      __syncthreads();  // the next user may hit the same columns from other threads
+    }
+    // compact the touched columns (every contribution is > 0) in ascending order
+    const double a = alpha[i];
+    const int64_t wbase = wt_ptr[i];
+    int base = 0;
+    for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
+      const int j = j0 + threadIdx.x;
+      const bool nz = j < tile && acc[j] != 0.0;
+      const uint64_t b = __ballot(nz);
+      const int w = threadIdx.x / 64;
+      if (lane_id() == 0) wsum[w] = __popcll(b);
+      __syncthreads();
+      int before_w = 0, total = 0;
+      for (int q = 0; q < 4; ++q) {
+        if (q < w) before_w += wsum[q];
+        total += wsum[q];
+      }
+      if (nz) {
+        const int item = item_begin + j;
+        double den = a * beta[item];
+        if (den == 0.0) den = 1.0;
+        const int pos = base + before_w + __popcll(b & lanemask_lt());
+        wt_col[wbase + pos] = item;
+        wt_val[wbase + pos] = acc[j] / den;
+      }
+      base += total;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) wt_len[i] = base;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ wt_ptr,
+                                                  int64_t n_items,
+                                                  unsigned long long *__restrict__ n_hub,
+                                                  int64_t *__restrict__ hub_rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  if (wt_ptr[i + 1] - wt_ptr[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
+}
+
+// F[u][j - j0] = sum over items(u) ascending of W[i][j]; one wave per user, RB rows in
+// flight. LDS: tile doubles per wave (dynamic).
+template <int RB>
+__global__ __launch_bounds__(256) void k_tile_resource(
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_users, const int64_t *__restrict__ wt_ptr, const int32_t *__restrict__ wt_len,
+    const int32_t *__restrict__ wt_col, const double *__restrict__ wt_val, int32_t item_begin,
+    int32_t tile, double *__restrict__ F, int64_t ldf) {
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int64_t u = (int64_t)blockIdx.x * (blockDim.x / 64) + wave;
+  if (u >= n_users) return;
+  double *acc = lds + (int64_t)wave * tile;
+  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
+  wave_sync();
+  const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
+  for (int64_t p0 = pb; p0 < pe; p0 += 64) {
+    // lane l: metadata of row p0 + l
+    int64_t rp = 0;
+    int rl = 0;
+    if (p0 + lane < pe) {
+      const int32_t i = user_items[p0 + lane];
+      rp = wt_ptr[i];
+      rl = wt_len[i];
+    }
+    const int nr = (pe - p0) < 64 ? (int)(pe - p0) : 64;
+    for (int r0 = 0; r0 < nr; r0 += RB) {
+      // RB rows' first 64 entries in flight together
+      int col[RB];
+      double val[RB];
+      int len[RB];
+      int64_t ptr[RB];
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        const int r = r0 + q;
+        len[q] = r < nr ? __shfl(rl, r) : 0;
+        ptr[q] = __shfl(rp, r < nr ? r : 0);
+        col[q] = 0;
+        val[q] = 0.0;
+        if (lane < len[q]) {
+          col[q] = wt_col[ptr[q] + lane];
+          val[q] = wt_val[ptr[q] + lane];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < RB; ++q) {
+        if (lane < len[q]) acc[col[q] - item_begin] += val[q];
+        for (int e = 64 + lane; e < len[q]; e += 64)  // long rows: rest of the entries
+          acc[wt_col[ptr[q] + e] - item_begin] += wt_val[ptr[q] + e];
+        wave_sync();  // the next row may hit the same columns from other lanes
+      }
+    }
+  }
+  double *row = F + u * ldf;
+  for (int j = lane; j < tile; j += 64) row[j] = acc[j];
+}
+
+template <int Q>
+__device__ __forceinline__ void load_frag(const float *__restrict__ p, float (&v)[Q]) {
+  const float4 *p4 = reinterpret_cast<const float4 *>(p);
+#pragma unroll
+  for (int t = 0; t < Q / 4; ++t) {
+    const float4 q = p4[t];
+    v[4 * t + 0] = q.x;
+    v[4 * t + 1] = q.y;
+    v[4 * t + 2] = q.z;
+    v[4 * t + 3] = q.w;
+  }
+}
+
+// Merge the tile's columns of (G *) F into running per-user top-K lists (io_val/io_idx,
+// sorted, index -1 = empty). D = 0: no G factor. One wave = NG groups of 16 users (rows);
+// lane (ul, gq) holds user ul of each group and items 4gq..4gq+3 of each 16-item step.
+template <int D, int NG, int M>
+__global__ __launch_bounds__(128) void k_tile_topk(
+    const double *__restrict__ F, int64_t ldf, int64_t n_rows, int32_t item_begin,
+    int32_t n_cols, const float *__restrict__ eu, const float *__restrict__ ei,
+    const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col, int drop,
+    int k, int first, double *__restrict__ io_val, int64_t *__restrict__ io_idx) {
+  constexpr int CAP = 64 * M;
+  constexpr int Q = D > 0 ? D / 4 : 1;
+  __shared__ double cs[2][NG][16][CAP];
+  __shared__ int ci[2][NG][16][CAP];
+  __shared__ int exs[2][64];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15, gq = lane >> 4;
+  const int64_t ubase = ((int64_t)blockIdx.x * 2 + wave) * (16 * NG);
+  if (ubase >= n_rows) return;
+
+  float uf[NG][Q];
+  bool uvalid[NG];
+  int cnt[NG], chk[NG];
+  double thr[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
+  const int lim_end = item_begin + n_cols;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t r = ubase + g * 16 + ul;
+    uvalid[g] = r < n_rows;
+    const int64_t rr = uvalid[g] ? r : n_rows - 1;
+    if (D > 0) load_frag<Q>(eu + rr * D + gq * Q, uf[g]);
+    ex_pos[g] = 0;
+    ex_hi[g] = 0;
+    if (drop && ex_rowptr && uvalid[g]) {
+      ex_hi[g] = ex_rowptr[r + 1];
+      ex_pos[g] = lower_bound_i32(ex_col, ex_rowptr[r], ex_hi[g], item_begin);
+    }
+    cnt[g] = 0;
+    chk[g] = 0;
+    thr[g] = uvalid[g] ? neg_inf<double>() : __builtin_huge_val();
+  }
+  // running lists -> LDS (already sorted and exclusion-checked)
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t r = ubase + g * 16 + u;
+      int nv = 0;
+      double last = neg_inf<double>();
+      if (!first && r < n_rows) {
+        for (int e0 = 0; e0 < k; e0 += 64) {
+          const int e = e0 + lane;
+          const int64_t id = e < k ? io_idx[r * k + e] : -1;
+          const bool ok = id >= 0;
+          if (ok) {
+            cs[wave][g][u][e] = io_val[r * k + e];
+            ci[wave][g][u][e] = (int)id;
+          }
+          nv += __popcll(__ballot(ok));
+        }
+        wave_sync();
+        if (nv == k) last = cs[wave][g][u][k - 1];
+      }
+      if (ul == u) {
+        cnt[g] = nv;
+        chk[g] = nv;
+        if (uvalid[g]) thr[g] = last;
+      }
+    }
+  }
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+
+  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
+    const int n = __shfl(cnt[g], u);
+    const int c0 = __shfl(chk[g], u);
+    int64_t pos = __shfl(ex_pos[g], u);
+    const int64_t hi = __shfl(ex_hi[g], u);
+    double *ks = &cs[wave][g][u][0];
+    int *is = &ci[wave][g][u][0];
+    if (n > c0) {
+      while (pos < hi) {  // excluded items in [previous limit, lim): drop their entries
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        const int nin = __popcll(__ballot(x < lim));
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        for (int j = c0 + lane; j < n; j += 64) {
+          const int item = is[j];
+          int a = 0, b = nin;
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) ks[j] = neg_inf<double>();
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
+      }
+    }
+    double t;
+    int tid;
+    const int nc = wave_compact<double, M>(ks, is, n, k, t, tid);
+    if (ul == u) {
+      cnt[g] = nc;
+      chk[g] = nc;
+      ex_pos[g] = pos;
+      thr[g] = !uvalid[g] ? __builtin_huge_val() : t;
+    }
+  };
+
+  for (int it = 0; it < n_cols; it += 16) {
+    double sc[NG][4];
+    if constexpr (D > 0) {
+      const int j = item_begin + it + ul;
+      const int jc = it + ul < n_cols ? j : item_begin + n_cols - 1;
+      float af[Q];
+      load_frag<Q>(ei + (int64_t)jc * D + gq * Q, af);
+      f32x4 acc[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < Q; ++s)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[g][r] = (double)acc[g][r];
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int64_t row = ubase + g * 16 + ul;
+      const int64_t rr = row < n_rows ? row : n_rows - 1;
+      const double *fr = F + rr * ldf + it + gq * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool in = it + gq * 4 + r < n_cols;
+        const double f = in ? fr[r] : 0.0;
+        const double v = D > 0 ? sc[g][r] * f : f;
+        const bool cand = in && v > thr[g];
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+          const int p = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][p] = v;
+            ci[wave][g][ul][p] = item_begin + it + gq * 4 + r;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    if (__ballot(over)) {
+      const int lim = item_begin + (it + 16 < n_cols ? it + 16 : n_cols);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+        if (need) {
+          wave_sync();
+          while (need) {
+            const int u = __ffsll((long long)need) - 1;
+            need &= need - 1;
+            compact_user(g, u, lim);
+          }
+        }
+      }
+    }
+  }
+
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t r = ubase + g * 16 + u;
+      if (r >= n_rows) break;
+      compact_user(g, u, lim_end);
+      const int nc = __shfl(cnt[g], u);
+      for (int e = lane; e < k; e += 64) {
+        const double v = e < nc ? cs[wave][g][u][e] : neg_inf<double>();
+        const bool ok = e < nc && v != neg_inf<double>();  // dropped entries never surface
+        io_val[r * k + e] = ok ? v : neg_inf<double>();
+        io_idx[r * k + e] = ok ? ci[wave][g][u][e] : -1;
+      }
+      wave_sync();
+    }
+  }
+}
+
+template <int D>
+static void launch_tile_topk(int M, const double *F, int64_t ldf, int64_t n_rows, int32_t j0,
+                             int32_t n_cols, const float *eu, const float *ei,
+                             const int64_t *ex_rowptr, const int32_t *ex_col, int drop, int k,
+                             int first, double *io_val, int64_t *io_idx, hipStream_t s) {
+  // LDS per block (2 waves): 2 * NG * 16 * CAP * 12 B = 48 KiB (M=1, NG=2), 48 KiB (M=2,
+  // NG=1), 96 KiB (M=4, NG=1)
+  if (M == 1) {
+    const unsigned b = (unsigned)((n_rows + 63) / 64);
+    k_tile_topk<D, 2, 1><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  } else if (M == 2) {
+    const unsigned b = (unsigned)((n_rows + 31) / 32);
+    k_tile_topk<D, 1, 2><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  } else {
+    const unsigned b = (unsigned)((n_rows + 31) / 32);
+    k_tile_topk<D, 1, 4><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  }
+}
+
+}  // namespace lg
+
+using namespace lg;
+
+extern "C" int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
+                                     double *alpha, double *beta, lg_stream_t stream) {
+  LG_REQUIRE(k_item && alpha && beta && n_items >= 0, "lg_hybrid_factors_f64: bad arguments");
+  if (n_items == 0) return LG_OK;
+  k_hybrid_factors<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream>>>(k_item, n_items, lambda, alpha, beta);
+  return launch_status("lg_hybrid_factors_f64");
+}
+
+extern "C" int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
+                                     int64_t n_users, int32_t item_end, const int64_t *cur,
+                                     int64_t *end, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && cur && end && n_users >= 0 && cur != end,
+             "lg_spread_tile_cursor: bad arguments");
+  if (n_users == 0) return LG_OK;
+  k_tile_cursor<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0,
+                  (hipStream_t)stream>>>(user_rowptr, user_items, n_users, item_end, cur, end);
+  return launch_status("lg_spread_tile_cursor");
+}
+
+extern "C" int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
+                                    int64_t n_items, const int64_t *cur, const int64_t *end,
+                                    int64_t *bound, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && cur && end && bound && n_items >= 0,
+             "lg_spread_tile_bound: bad arguments");
+  if (n_items == 0) return LG_OK;
+  k_tile_bound<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
+      item_rowptr, item_users, n_items, cur, end, bound);
+  return launch_status("lg_spread_tile_bound");
+}
+
+extern "C" size_t lg_spread_tile_weight_ws_bytes(int64_t n_items) {
+  return (size_t)(n_items + 1) * sizeof(int64_t);  // hub count + hub row list
+}
+
+extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                                         const int64_t *user_rowptr, const int32_t *user_items,
+                                         int64_t n_items, const int64_t *cur,
+                                         const int64_t *end, const double *alpha,
+                                         const double *beta, int32_t item_begin, int32_t tile,
+                                         const int64_t *wt_ptr, int32_t *wt_col,
+                                         double *wt_val, int32_t *wt_len, void *ws,
+                                         size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_rowptr && cur && end && alpha && beta && wt_ptr && wt_len &&
+                 n_items >= 0,
+             "lg_spread_tile_weight_f64: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && item_begin >= 0,
+             "lg_spread_tile_weight_f64: tile %d not in [1, 8192]", tile);
+  if (n_items == 0) return LG_OK;
+  const size_t need = lg_spread_tile_weight_ws_bytes(n_items);
+  if (!ws || ws_bytes < need) {
+    set_error("lg_spread_tile_weight_f64: workspace %zu < %zu bytes", ws_bytes, need);
+    return LG_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *n_hub = (int64_t *)ws;
+  int64_t *hub_rows = n_hub + 1;
+  if (hipMemsetAsync(n_hub, 0, sizeof(int64_t), s) != hipSuccess) {
+    set_error("lg_spread_tile_weight_f64: hipMemsetAsync failed");
+    return LG_ERR_HIP;
+  }
+  const unsigned rb = (unsigned)((n_items + 3) / 4);
+  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_rowptr,
+                                               user_items, n_items, cur, end, alpha, beta,
+                                               wt_ptr, wt_col, wt_val, wt_len);
+  k_hub_list<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
+      wt_ptr, n_items, (unsigned long long *)n_hub, hub_rows);
+  k_tile_weight_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
+      hub_rows, n_hub, item_rowptr, item_users, user_rowptr, user_items, cur, end, alpha, beta,
+      item_begin, tile, wt_ptr, wt_col, wt_val, wt_len);
+  return launch_status("lg_spread_tile_weight_f64");
+}
+
+extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
+                                           const int32_t *user_items, int64_t n_users,
+                                           const int64_t *wt_ptr, const int32_t *wt_len,
+                                           const int32_t *wt_col, const double *wt_val,
+                                           int32_t item_begin, int32_t tile, double *F,
+                                           int64_t ldf, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && wt_ptr && wt_len && F && n_users >= 0 && ldf >= tile,
+             "lg_spread_tile_resource_f64: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192, "lg_spread_tile_resource_f64: tile %d not in [1, 8192]",
+             tile);
+  if (n_users == 0) return LG_OK;
+  // 4 waves per block, tile doubles of LDS per wave (<= 64 KiB per wave at tile 8192)
+  const int waves = tile <= 2048 ? 4 : (tile <= 4096 ? 2 : 1);
+  const size_t lds = (size_t)waves * tile * sizeof(double);
+  k_tile_resource<8><<<dim3((unsigned)((n_users + waves - 1) / waves)), dim3(64 * waves), lds,
+                       (hipStream_t)stream>>>(user_rowptr, user_items, n_users, wt_ptr, wt_len,
+                                              wt_col, wt_val, item_begin, tile, F, ldf);
+  return launch_status("lg_spread_tile_resource_f64");
+}
+
+extern "C" int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows,
+                                int32_t item_begin, int32_t n_cols, const float *eu,
+                                const float *ei, int32_t dim, const int64_t *ex_rowptr,
+                                const int32_t *ex_col, int32_t excl_mode, int32_t k,
+                                int32_t first, double *io_val, int64_t *io_idx,
+                                lg_stream_t stream) {
+  LG_REQUIRE(F && io_val && io_idx && n_rows >= 0 && n_cols >= 1 && ldf >= n_cols &&
+                 item_begin >= 0 && (int64_t)item_begin + n_cols < 0x7fffffff,
+             "lg_tile_topk_f64: bad arguments");
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_tile_topk_f64: k=%d not in [1,128]", k);
+  LG_REQUIRE(!eu == !ei, "lg_tile_topk_f64: eu/ei must both be set or both NULL");
+  LG_REQUIRE(!eu || dim == 32 || dim == 64 || dim == 128,
+             "lg_tile_topk_f64: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(excl_mode == LG_EXCL_DROP || excl_mode == LG_EXCL_NONE,
+             "lg_tile_topk_f64: bad excl_mode %d", excl_mode);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_tile_topk_f64: ex_rowptr/ex_col must both be set");
+  LG_REQUIRE(!(eu && excl_mode == LG_EXCL_NONE && ex_rowptr),
+             "lg_tile_topk_f64: a G factor with exclusions requires LG_EXCL_DROP");
+  if (n_rows == 0) return LG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int M = k <= 32 ? 1 : (k <= 64 ? 2 : 4);
+  const int drop = excl_mode == LG_EXCL_DROP;
+  switch (eu ? dim : 0) {
+    case 0: launch_tile_topk<0>(M, F, ldf, n_rows, item_begin, n_cols, eu, ei, ex_rowptr, ex_col, drop, k, first, io_val, io_idx, s); break;
+    case 32: launch_tile_topk<32>(M, F, ldf, n_rows, item_begin, n_cols, eu, ei, ex_rowptr, ex_col, drop, k, first, io_val, io_idx, s); break;
+    case 64: launch_tile_topk<64>(M, F, ldf, n_rows, item_begin, n_cols, eu, ei, ex_rowptr, ex_col, drop, k, first, io_val, io_idx, s); break;
+    default: launch_tile_topk<128>(M, F, ldf, n_rows, item_begin, n_cols, eu, ei, ex_rowptr, ex_col, drop, k, first, io_val, io_idx, s); break;
+  }
+  return launch_status("lg_tile_topk_f64");
+}

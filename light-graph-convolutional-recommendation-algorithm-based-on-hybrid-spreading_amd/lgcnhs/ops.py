@@ -8,6 +8,8 @@ hybrid_weight    HybridS W                         model/SpreadMethod/model.py:6
 spread_resource  F = A @ W                         model/SpreadMethod/model.py:88-99
 rows_topk        argsort + filter + [:k], G * F    model/SpreadMethod/recommend.py:31-50,
                                                    model/SpreadLightGCN/model.py:151
+spread_topk_tiled  the above over item tiles,      (same; for catalogs whose I x I W
+                   never holding an I x I matrix    does not fit)
 """
 from __future__ import annotations
 
@@ -291,4 +293,130 @@ def spread_topk(A: Interactions, W: torch.Tensor, k: int, excl: RowSets | None,
         ex = excl.slice_rows(u0, u1) if excl is not None else None
         v, i = rows_topk(Fb, k, ex, drop, None if eu is None else eu[u0:u1], ei)
         vals[u0:u1], idxs[u0:u1] = v, i
+    return vals, idxs
+
+
+# ------------------------------------------------------------------- factored spreading
+def hybrid_factors(k_item: torch.Tensor, lam: float):
+    """(alpha, beta) = (k_i^(1-lambda), k_i^lambda), the HybridS degree factors."""
+    k_item = k_item.contiguous().to(torch.float64)
+    n = k_item.shape[0]
+    alpha = torch.empty(n, dtype=torch.float64, device=k_item.device)
+    beta = torch.empty_like(alpha)
+    N.check(N.lib().lg_hybrid_factors_f64(N.ptr(k_item), n, float(lam), N.ptr(alpha),
+                                          N.ptr(beta), N.stream_handle(k_item.device)),
+            "lg_hybrid_factors_f64")
+    return alpha, beta
+
+
+class TileWeights:
+    """W = HybridS(general_W) restricted to one item tile, row-major over all items
+    (lg_spread_tile_* of include/lgcnhs.h). ``advance()`` moves to the next tile; the
+    buffers are reused and grown on demand."""
+
+    def __init__(self, A: Interactions, lam: float, tile: int):
+        if not 1 <= tile <= 8192:
+            raise ValueError(f"tile {tile} not in [1, 8192]")
+        self.A, self.tile = A, int(tile)
+        dev = A.k_item.device
+        self.dev = dev
+        self.alpha, self.beta = hybrid_factors(A.k_item, lam)
+        I = A.n_items
+        self.cur = A.by_user.rowptr[:-1].contiguous().clone()
+        self.end = torch.empty_like(self.cur)
+        self.bound = torch.empty(I, dtype=torch.int64, device=dev)
+        self.ptr = torch.zeros(I + 1, dtype=torch.int64, device=dev)
+        self.len = torch.empty(I, dtype=torch.int32, device=dev)
+        self.ws = torch.empty(max(1, N.lib().lg_spread_tile_weight_ws_bytes(I)),
+                              dtype=torch.uint8, device=dev)
+        self.col = torch.empty(0, dtype=torch.int32, device=dev)
+        self.val = torch.empty(0, dtype=torch.float64, device=dev)
+        self.j0 = None
+        self.width = 0
+
+    def build(self, j0: int) -> None:
+        """Build the tile [j0, j0 + tile); tiles must come in ascending order from 0."""
+        A, I, L = self.A, self.A.n_items, N.lib()
+        strm = N.stream_handle(self.dev)
+        if j0 == 0:
+            self.cur.copy_(A.by_user.rowptr[:-1])
+        elif self.j0 is None or j0 != self.j0 + self.tile:
+            raise ValueError("tiles must be built in ascending order")
+        else:
+            self.cur, self.end = self.end, self.cur
+        width = min(self.tile, I - j0)
+        N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
+                                        A.n_users, j0 + width, N.ptr(self.cur),
+                                        N.ptr(self.end), strm), "lg_spread_tile_cursor")
+        N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
+                                       N.ptr(self.cur), N.ptr(self.end), N.ptr(self.bound),
+                                       strm), "lg_spread_tile_bound")
+        torch.cumsum(self.bound, 0, out=self.ptr[1:])
+        total = int(self.ptr[-1])  # host sync: sizes the row storage
+        if total > self.col.numel():
+            cap = max(total, int(self.col.numel() * 1.25))
+            self.col = torch.empty(cap, dtype=torch.int32, device=self.dev)
+            self.val = torch.empty(cap, dtype=torch.float64, device=self.dev)
+        N.check(L.lg_spread_tile_weight_f64(
+            N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.rowptr),
+            N.ptr(A.by_user.col), I, N.ptr(self.cur), N.ptr(self.end), N.ptr(self.alpha),
+            N.ptr(self.beta), j0, self.tile, N.ptr(self.ptr), N.ptr(self.col),
+            N.ptr(self.val), N.ptr(self.len), N.ptr(self.ws), self.ws.numel(), strm),
+            "lg_spread_tile_weight_f64")
+        self.j0, self.width = j0, width
+
+    def resource(self, u0: int, u1: int, out: torch.Tensor) -> torch.Tensor:
+        """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
+        A = self.A
+        N.check(N.lib().lg_spread_tile_resource_f64(
+            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), u1 - u0, N.ptr(self.ptr),
+            N.ptr(self.len), N.ptr(self.col), N.ptr(self.val), self.j0, self.tile, N.ptr(out),
+            out.stride(0), N.stream_handle(self.dev)), "lg_spread_tile_resource_f64")
+        return out
+
+
+def tile_topk(F: torch.Tensor, j0: int, n_cols: int, k: int, vals: torch.Tensor,
+              idxs: torch.Tensor, first: bool, excl: RowSets | None = None, drop: bool = True,
+              eu: torch.Tensor | None = None, ei: torch.Tensor | None = None) -> None:
+    """Merge columns [j0, j0 + n_cols) of (G *) F into the running lists vals/idxs."""
+    n = F.shape[0]
+    d = 0
+    if eu is not None:
+        eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
+        d = eu.shape[1]
+    N.check(N.lib().lg_tile_topk_f64(
+        N.ptr(F), F.stride(0), n, j0, n_cols, N.ptr(eu), N.ptr(ei), d,
+        N.ptr(excl.rowptr if excl else None), N.ptr(excl.col if excl else None),
+        N.LG_EXCL_DROP if drop else N.LG_EXCL_NONE, int(k), int(bool(first)), N.ptr(vals),
+        N.ptr(idxs), N.stream_handle(F.device)), "lg_tile_topk_f64")
+
+
+def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
+                      drop: bool = True, eu: torch.Tensor | None = None,
+                      ei: torch.Tensor | None = None, users: slice | None = None,
+                      tile: int = 2048, block_users: int | None = None):
+    """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
+    never holds general_W, W (I x I) or F (U x I). Bitwise the result of
+    spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
+    ``users`` restricts the output to a row range (the multi-GPU shard)."""
+    u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
+    n = u1 - u0
+    dev = A.k_item.device
+    vals = torch.full((n, k), float("-inf"), dtype=torch.float64, device=dev)
+    idxs = torch.full((n, k), -1, dtype=torch.int64, device=dev)
+    if n == 0 or A.n_items == 0:
+        return vals, idxs
+    if block_users is None:
+        block_users = max(1, min(n, (1 << 30) // (tile * 8)))  # ~1 GiB of F per block
+    F = torch.empty((min(block_users, n), tile), dtype=torch.float64, device=dev)
+    tw = TileWeights(A, lam, tile)
+    ex = excl.slice_rows(u0, u1) if excl is not None else None
+    for j0 in range(0, A.n_items, tile):
+        tw.build(j0)
+        for b0 in range(0, n, block_users):
+            b1 = min(n, b0 + block_users)
+            Fb = tw.resource(u0 + b0, u0 + b1, F[: b1 - b0])
+            tile_topk(Fb, j0, tw.width, k, vals[b0:b1], idxs[b0:b1], j0 == 0,
+                      ex.slice_rows(b0, b1) if ex is not None else None, drop,
+                      None if eu is None else eu[u0 + b0:u0 + b1], ei)
     return vals, idxs

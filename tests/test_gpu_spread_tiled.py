@@ -1,0 +1,124 @@
+"""GPU parity of the factored (item-tiled) spreading path, K3s: bitwise
+equal to the dense path (lg_spread_general_f64 -> lg_hybrid_weight_f64 ->
+lg_spread_resource_f64 -> lg_rows_topk_f64), which is itself pinned to the reference's numpy
+results in test_gpu_spread.py; plus the reference fixture for the LGCNHS recommendation."""
+import numpy as np
+import pytest
+import torch
+
+from _compare import compare_topk_sets
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _inter(U, I, n, seed, zipf=False):
+    from lgcnhs import ops
+    from lgcnhs.synth import synth_interactions
+    u, i = synth_interactions(U, I, n, seed=seed, dist="zipf" if zipf else "uniform")
+    return ops.Interactions.from_pairs(torch.as_tensor(u), torch.as_tensor(i), U, I, DEV)
+
+
+def _dense_tile(tw, I):
+    """The current tile of W as a dense [I, width] matrix (zeros where no entry)."""
+    ptr, ln = tw.ptr.cpu().numpy(), tw.len.cpu().numpy()
+    col, val = tw.col.cpu().numpy(), tw.val.cpu().numpy()
+    out = np.zeros((I, tw.width))
+    for i in range(I):
+        c = col[ptr[i]:ptr[i] + ln[i]]
+        assert np.all(np.diff(c) > 0), "row entries must be ascending and unique"
+        assert np.all((c >= tw.j0) & (c < tw.j0 + tw.width))
+        out[i, c - tw.j0] = val[ptr[i]:ptr[i] + ln[i]]
+    return out
+
+
+@pytest.mark.parametrize("zipf", [False, True])
+@pytest.mark.parametrize("lam", [0.0, 0.5, 0.85, 1.0])
+def test_tile_weights_and_resource_bitwise(zipf, lam):
+    """Every tile of W and of F equals the dense matrices' columns bit for bit (the hub rows
+    of the zipf graph exceed the 256-pair in-wave sort and take the block-wide path)."""
+    from lgcnhs import ops
+    U, I = 700, 900
+    A = _inter(U, I, 30000 if zipf else 12000, seed=5, zipf=zipf)
+    W = ops.hybrid_weight(ops.spread_general(A), A.k_item, lam).cpu().numpy()
+    F = ops.spread_resource(A, torch.as_tensor(W).to(DEV)).cpu().numpy()
+    tile = 256
+    tw = ops.TileWeights(A, lam, tile)
+    Fb = torch.empty((U, tile), dtype=torch.float64, device=DEV)
+    hub_seen = False
+    for j0 in range(0, I, tile):
+        tw.build(j0)
+        hub_seen |= bool((tw.bound > 256).any())
+        Wt = _dense_tile(tw, I)
+        assert np.array_equal(Wt.view(np.uint64), W[:, j0:j0 + tw.width].view(np.uint64))
+        tw.resource(0, U, Fb)
+        Ft = Fb[:, :tw.width].cpu().numpy()
+        assert np.array_equal(Ft.view(np.uint64), F[:, j0:j0 + tw.width].view(np.uint64))
+    if zipf:
+        assert hub_seen, "the zipf graph should exercise the hub-row path"
+
+
+@pytest.mark.parametrize("k", [1, 10, 33, 100])
+@pytest.mark.parametrize("tile", [64, 333, 4096])
+@pytest.mark.parametrize("mode", ["G_drop", "drop", "none"])
+def test_spread_topk_tiled_equals_dense(k, tile, mode):
+    from lgcnhs import ops
+    U, I, d = 300, 1000, 64
+    A = _inter(U, I, 9000, seed=11, zipf=True)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
+    ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
+    use_g = mode == "G_drop"
+    drop = mode != "none"
+    lam = 0.4
+    W = ops.hybrid_weight(ops.spread_general(A), A.k_item, lam)
+    kw = dict(eu=eu if use_g else None, ei=ei if use_g else None)
+    v0, i0 = ops.spread_topk(A, W, k, A.by_user, drop=drop, **kw)
+    v1, i1 = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile,
+                                   block_users=128, **kw)
+    assert torch.equal(i1, i0)
+    assert torch.equal(v1.view(torch.int64), v0.view(torch.int64))
+
+
+def test_spread_topk_tiled_user_shards():
+    """users= slices (the multi-GPU shard) give the rows of the full run."""
+    from lgcnhs import ops
+    U, I = 500, 700
+    A = _inter(U, I, 10000, seed=2)
+    v, i = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=200)
+    for a, b in ((0, 130), (130, 131), (131, 500)):
+        vs, is_ = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, users=slice(a, b), tile=200)
+        assert torch.equal(is_, i[a:b]) and torch.equal(vs, v[a:b])
+
+
+def test_spread_lightgcn_tiled_vs_reference(golden):
+    """The tiled LGCNHS recommendation against the reference fixture (getResourceMat +
+    recommendForAllUser of model/SpreadLightGCN)."""
+    import pandas as pd
+    from lgcnhs import ops
+    from model.LightGCN.model import LightGCN
+    g = golden("lightgcn_mid")
+    U, I, k = int(g["n_users"]), int(g["n_items"]), int(g["k"])
+    torch.manual_seed(42)
+    m = LightGCN(U, I, 64, 3).to(DEV)
+    both = np.concatenate([g["train"], g["val"]], axis=1).astype(np.int64)
+    A = ops.Interactions.from_pairs(torch.as_tensor(both[0]), torch.as_tensor(both[1]), U, I,
+                                    DEV)
+    eu = m.users_emb.weight.detach().float().contiguous()
+    ei = m.items_emb.weight.detach().float().contiguous()
+    _, idx = ops.spread_topk_tiled(A, float(g["slgcn_lambda"]), k, A.by_user, eu=eu, ei=ei,
+                                   tile=512)
+    gaps = g["slgcn_gaps"]
+    compare_topk_sets(idx.cpu().numpy(), g["slgcn_recs"], gaps,
+                      tol=1e-6 * np.nanmax(np.abs(gaps)))
+
+
+def test_tile_api_errors():
+    from lgcnhs import ops
+    A = _inter(50, 60, 500, seed=1)
+    with pytest.raises(ValueError):
+        ops.TileWeights(A, 0.5, 0)
+    tw = ops.TileWeights(A, 0.5, 16)
+    tw.build(0)
+    with pytest.raises(ValueError):
+        tw.build(48)  # not the next tile
