@@ -207,32 +207,38 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
 int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
                           double *alpha, double *beta, lg_stream_t stream);
 
+/* inv[v] = fl(1 / (rowptr[v+1] - rowptr[v])): the (A.T / k_u) factor of
+ * model/SpreadMethod/model.py:21-25, as lg_spread_general_f64 computes it. */
+int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *inv,
+                      lg_stream_t stream);
+
 /* end[v] = first position p >= cur[v] of user v's item row (user_rowptr/user_items, items
- * ascending) with user_items[p] >= item_end (or the row end). With cur = the row starts
- * (first tile) or the previous tile's end, user_items[cur[v] .. end[v]) are v's items in
- * the tile. cur and end must not alias. */
+ * ascending) with user_items[p] >= item_end (or the row end), count[v] = end[v] - cur[v].
+ * With cur = the row starts (first tile) or the previous tile's end,
+ * user_items[cur[v] .. end[v]) are v's items in the tile. cur and end must not alias;
+ * item_end - (the tile's first item) <= 8192 (count is 16-bit). */
 int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                           int64_t n_users, int32_t item_end, const int64_t *cur,
-                          int64_t *end, lg_stream_t stream);
+                          int64_t *end, uint16_t *count, lg_stream_t stream);
 
-/* bound[i] = sum over users v of item i (item_rowptr/item_users) of end[v] - cur[v]:
- * the number of (user, tile item) pairs behind W's row i in the tile, an upper bound on the
- * row's entries. */
+/* bound[i] = sum over users v of item i (item_rowptr/item_users) of count[v]: the number of
+ * (user, tile item) pairs behind W's row i in the tile, an upper bound on its entries. */
 int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
-                         int64_t n_items, const int64_t *cur, const int64_t *end,
-                         int64_t *bound, lg_stream_t stream);
+                         int64_t n_items, const uint16_t *count, int64_t *bound,
+                         lg_stream_t stream);
 
 /* Row i of W restricted to the tile, for every item i:
- *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} fl(1 / k_v))
+ *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} inv_deg[v])
  *             / (alpha[i] * beta[j])          (den == 0 -> 1)
  * written at wt_col/wt_val[wt_ptr[i] .. wt_ptr[i] + wt_len[i]) in ascending j, where
  * wt_ptr[n_items + 1] is the exclusive prefix of lg_spread_tile_bound's bounds (row
- * capacities). ws: lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in
+ * capacities); cur/count from lg_spread_tile_cursor, inv_deg from lg_inv_degree_f64 over
+ * the user rows. ws: lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in
  * [1, 8192]; every item of the tile must lie in [item_begin, item_begin + tile). */
 size_t lg_spread_tile_weight_ws_bytes(int64_t n_items);
 int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                              const int64_t *user_rowptr, const int32_t *user_items,
-                              int64_t n_items, const int64_t *cur, const int64_t *end,
+                              const int32_t *user_items, const double *inv_deg,
+                              int64_t n_items, const int64_t *cur, const uint16_t *count,
                               const double *alpha, const double *beta, int32_t item_begin,
                               int32_t tile, const int64_t *wt_ptr, int32_t *wt_col,
                               double *wt_val, int32_t *wt_len, void *ws, size_t ws_bytes,

@@ -45,34 +45,41 @@ __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict
   beta[i] = pow(k_item[i], lambda);
 }
 
+__global__ __launch_bounds__(256) void k_inv_degree(const int64_t *__restrict__ rowptr,
+                                                    int64_t n, double *__restrict__ inv) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  inv[v] = 1.0 / (double)(rowptr[v + 1] - rowptr[v]);  // k_spread_general's fl(1/k_v)
+}
+
 __global__ __launch_bounds__(256) void k_tile_cursor(const int64_t *__restrict__ user_rowptr,
                                                      const int32_t *__restrict__ user_items,
                                                      int64_t n_users, int32_t item_end,
                                                      const int64_t *__restrict__ cur,
-                                                     int64_t *__restrict__ end) {
+                                                     int64_t *__restrict__ end,
+                                                     uint16_t *__restrict__ count) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_users) return;
-  int64_t p = cur[v];
+  const int64_t p0 = cur[v];
+  int64_t p = p0;
   const int64_t pe = user_rowptr[v + 1];
   while (p < pe && user_items[p] < item_end) ++p;
   end[v] = p;
+  count[v] = (uint16_t)(p - p0);  // <= tile <= 8192
 }
 
 // one wave per item row
 __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ item_rowptr,
                                                     const int32_t *__restrict__ item_users,
                                                     int64_t n_items,
-                                                    const int64_t *__restrict__ cur,
-                                                    const int64_t *__restrict__ end,
+                                                    const uint16_t *__restrict__ count,
                                                     int64_t *__restrict__ bound) {
   const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   if (i >= n_items) return;
   const int lane = lane_id();
   int64_t s = 0;
-  for (int64_t e = item_rowptr[i] + lane; e < item_rowptr[i + 1]; e += 64) {
-    const int32_t v = item_users[e];
-    s += end[v] - cur[v];
-  }
+  for (int64_t e = item_rowptr[i] + lane; e < item_rowptr[i + 1]; e += 64)
+    s += count[item_users[e]];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (lane == 0) bound[i] = s;
@@ -80,12 +87,13 @@ __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ 
 
 constexpr int kSortMax = 256;  // pairs per row handled by the in-wave sort
 
-// Sort the n (<= 64*M) staged pairs (key = -item, id = user) of this wave, then reduce runs
-// of equal items in ascending user order and write the row.
+// Sort the n (<= 64*M) staged pairs (key = -item, id = staging position, which ascends
+// with the user) of this wave, then reduce runs of equal items in ascending user order
+// (weights sw[position] = fl(1/k_v)) and write the row.
 template <int M>
-__device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, int n, int64_t wbase,
-                                               const int64_t *__restrict__ user_rowptr,
-                                               double alpha_i, const double *__restrict__ beta,
+__device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, const double *sw, int n,
+                                               int64_t wbase, double alpha_i,
+                                               const double *__restrict__ beta,
                                                int32_t *__restrict__ wt_col,
                                                double *__restrict__ wt_val) {
   const int lane = lane_id();
@@ -116,10 +124,7 @@ __device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, int n, int64
       // run e, e+1, ... of one item, users ascending: 0.0 + w0 + w1 + ... in that order
       const int item = -skey[e];
       double s = 0.0;
-      for (int m = e; m < n && skey[m] == skey[e]; ++m) {
-        const int32_t v = sid[m];
-        s += 1.0 / (double)(user_rowptr[v + 1] - user_rowptr[v]);
-      }
+      for (int m = e; m < n && skey[m] == skey[e]; ++m) s += sw[sid[m]];
       double den = alpha_i * beta[item];
       if (den == 0.0) den = 1.0;
       const int pos = base + __popcll(hb & lanemask_lt());
@@ -134,13 +139,14 @@ __device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, int n, int64
 // one wave per item row; LDS staging of kSortMax pairs per wave
 __global__ __launch_bounds__(256) void k_tile_weight(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
-    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_items, const int64_t *__restrict__ cur, const int64_t *__restrict__ end,
+    const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
+    int64_t n_items, const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
     const double *__restrict__ alpha, const double *__restrict__ beta,
     const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
     double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
   __shared__ int skey[4][kSortMax];
   __shared__ int sid[4][kSortMax];
+  __shared__ double sw[4][kSortMax];
   const int wave = threadIdx.x / 64;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   if (i >= n_items) return;
@@ -157,13 +163,11 @@ __global__ __launch_bounds__(256) void k_tile_weight(
   for (int64_t e0 = item_rowptr[i]; e0 < item_rowptr[i + 1]; e0 += 64) {
     const int64_t e = e0 + lane;
     int32_t v = 0;
-    int64_t s = 0, t = 0;
+    int c = 0;
     if (e < item_rowptr[i + 1]) {
       v = item_users[e];
-      s = cur[v];
-      t = end[v];
+      c = count[v];
     }
-    const int c = (int)(t - s);
     // exclusive prefix of c over the lanes
     int pre = c;
 #pragma unroll
@@ -173,22 +177,28 @@ __global__ __launch_bounds__(256) void k_tile_weight(
     }
     const int total = __shfl(pre, 63);
     pre -= c;
-    for (int q = 0; q < c; ++q) {
-      skey[wave][n + pre + q] = -user_items[s + q];
-      sid[wave][n + pre + q] = v;
+    if (c) {
+      const int64_t s0 = cur[v];
+      const double w = inv_deg[v];
+      for (int q = 0; q < c; ++q) {
+        const int p = n + pre + q;
+        skey[wave][p] = -user_items[s0 + q];
+        sid[wave][p] = p;
+        sw[wave][p] = w;
+      }
     }
     n += total;
   }
   wave_sync();
   int len;
   if (n <= 64)
-    len = sort_reduce_row<1>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+    len = sort_reduce_row<1>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
                              wt_col, wt_val);
   else if (n <= 128)
-    len = sort_reduce_row<2>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+    len = sort_reduce_row<2>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
                              wt_col, wt_val);
   else
-    len = sort_reduce_row<4>(skey[wave], sid[wave], n, wbase, user_rowptr, alpha[i], beta,
+    len = sort_reduce_row<4>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
                              wt_col, wt_val);
   if (lane == 0) wt_len[i] = len;
 }
@@ -199,8 +209,8 @@ __global__ __launch_bounds__(256) void k_tile_weight(
 __global__ __launch_bounds__(256) void k_tile_weight_hub(
     const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
-    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    const int64_t *__restrict__ cur, const int64_t *__restrict__ end,
+    const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
+    const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
     const double *__restrict__ alpha, const double *__restrict__ beta, int32_t item_begin,
     int32_t tile, const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
     double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
@@ -213,9 +223,11 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
     __syncthreads();
     for (int64_t e = item_rowptr[i]; e < item_rowptr[i + 1]; ++e) {
       const int32_t v = item_users[e];
-      const double wv = 1.0 / (double)(user_rowptr[v + 1] - user_rowptr[v]);
-      for (int64_t p = cur[v] + threadIdx.x; p < end[v]; p += blockDim.x)
-        acc[user_items[p] - item_begin] += wv;
+      const int c = count[v];
+      if (c == 0) continue;  // uniform across the block: no barrier skipped unevenly
+      const double wv = inv_deg[v];
+      const int64_t s0 = cur[v];
+      for (int q = threadIdx.x; q < c; q += blockDim.x) acc[user_items[s0 + q] - item_begin] += wv;
       __syncthreads();  // the next user may hit the same columns from other threads
     }
     // compact the touched columns (every contribution is > 0) in ascending order
@@ -443,13 +455,27 @@ __global__ __launch_bounds__(128) void k_tile_topk(
     }
   };
 
-  for (int it = 0; it < n_cols; it += 16) {
-    double sc[NG][4];
+  // One 16-column step: the item fragment and the F values (clamped to valid memory, so
+  // every step issues the same loads) are loaded one step ahead.
+  auto load_step = [&](int it, float(&af)[Q], double(&f)[NG][4]) __attribute__((always_inline)) {
     if constexpr (D > 0) {
-      const int j = item_begin + it + ul;
-      const int jc = it + ul < n_cols ? j : item_begin + n_cols - 1;
-      float af[Q];
+      const int jc = it + ul < n_cols ? item_begin + it + ul : item_begin + n_cols - 1;
       load_frag<Q>(ei + (int64_t)jc * D + gq * Q, af);
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int64_t row = ubase + g * 16 + ul;
+      const double *fr = F + (row < n_rows ? row : n_rows - 1) * ldf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = it + gq * 4 + r;
+        f[g][r] = fr[c < n_cols ? c : n_cols - 1];
+      }
+    }
+  };
+  auto process = [&](int it, const float(&af)[Q], const double(&f)[NG][4]) __attribute__((always_inline)) {
+    double v[NG][4];
+    if constexpr (D > 0) {
       f32x4 acc[NG];
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -461,27 +487,35 @@ __global__ __launch_bounds__(128) void k_tile_topk(
 #pragma unroll
       for (int g = 0; g < NG; ++g)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sc[g][r] = (double)acc[g][r];
+        for (int r = 0; r < 4; ++r) v[g][r] = (double)acc[g][r] * f[g][r];
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[g][r] = f[g][r];
     }
+    // fast filter: one ballot per step; the exact per-column insertion only on a hit
+    const int c0 = it + gq * 4;
+    bool any = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int64_t row = ubase + g * 16 + ul;
-      const int64_t rr = row < n_rows ? row : n_rows - 1;
-      const double *fr = F + rr * ldf + it + gq * 4;
+    for (int g = 0; g < NG; ++g)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool in = it + gq * 4 + r < n_cols;
-        const double f = in ? fr[r] : 0.0;
-        const double v = D > 0 ? sc[g][r] * f : f;
-        const bool cand = in && v > thr[g];
-        const uint64_t bal = __ballot(cand);
-        if (bal) {
-          const int p = cnt[g] + __popcll(bal & same_user & lanemask_lt());
-          if (cand) {
-            cs[wave][g][ul][p] = v;
-            ci[wave][g][ul][p] = item_begin + it + gq * 4 + r;
+      for (int r = 0; r < 4; ++r) any |= v[g][r] > thr[g];
+    if (__ballot(any)) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool cand = c0 + r < n_cols && v[g][r] > thr[g];
+          const uint64_t bal = __ballot(cand);
+          if (bal) {
+            const int p = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+            if (cand) {
+              cs[wave][g][ul][p] = v[g][r];
+              ci[wave][g][ul][p] = item_begin + c0 + r;
+            }
+            cnt[g] += __popcll(bal & same_user);
           }
-          cnt[g] += __popcll(bal & same_user);
         }
       }
     }
@@ -503,6 +537,18 @@ __global__ __launch_bounds__(128) void k_tile_topk(
         }
       }
     }
+  };
+
+  float afA[Q], afB[Q];
+  double fA[NG][4], fB[NG][4];
+  load_step(0, afA, fA);
+  for (int it = 0;; it += 32) {
+    load_step(it + 16, afB, fB);  // clamped: harmless past the end
+    process(it, afA, fA);
+    if (it + 16 >= n_cols) break;
+    load_step(it + 32, afA, fA);
+    process(it + 16, afB, fB);
+    if (it + 32 >= n_cols) break;
   }
 
   wave_sync();
@@ -559,25 +605,35 @@ extern "C" int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, doub
   return launch_status("lg_hybrid_factors_f64");
 }
 
+extern "C" int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *inv,
+                                 lg_stream_t stream) {
+  LG_REQUIRE(rowptr && inv && n_rows >= 0, "lg_inv_degree_f64: bad arguments");
+  if (n_rows == 0) return LG_OK;
+  k_inv_degree<<<dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
+      rowptr, n_rows, inv);
+  return launch_status("lg_inv_degree_f64");
+}
+
 extern "C" int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                                      int64_t n_users, int32_t item_end, const int64_t *cur,
-                                     int64_t *end, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && cur && end && n_users >= 0 && cur != end,
+                                     int64_t *end, uint16_t *count, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && cur && end && count && n_users >= 0 && cur != end,
              "lg_spread_tile_cursor: bad arguments");
   if (n_users == 0) return LG_OK;
   k_tile_cursor<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0,
-                  (hipStream_t)stream>>>(user_rowptr, user_items, n_users, item_end, cur, end);
+                  (hipStream_t)stream>>>(user_rowptr, user_items, n_users, item_end, cur, end,
+                                         count);
   return launch_status("lg_spread_tile_cursor");
 }
 
 extern "C" int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
-                                    int64_t n_items, const int64_t *cur, const int64_t *end,
-                                    int64_t *bound, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && cur && end && bound && n_items >= 0,
+                                    int64_t n_items, const uint16_t *count, int64_t *bound,
+                                    lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && count && bound && n_items >= 0,
              "lg_spread_tile_bound: bad arguments");
   if (n_items == 0) return LG_OK;
   k_tile_bound<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
-      item_rowptr, item_users, n_items, cur, end, bound);
+      item_rowptr, item_users, n_items, count, bound);
   return launch_status("lg_spread_tile_bound");
 }
 
@@ -586,14 +642,14 @@ extern "C" size_t lg_spread_tile_weight_ws_bytes(int64_t n_items) {
 }
 
 extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                                         const int64_t *user_rowptr, const int32_t *user_items,
+                                         const int32_t *user_items, const double *inv_deg,
                                          int64_t n_items, const int64_t *cur,
-                                         const int64_t *end, const double *alpha,
+                                         const uint16_t *count, const double *alpha,
                                          const double *beta, int32_t item_begin, int32_t tile,
                                          const int64_t *wt_ptr, int32_t *wt_col,
                                          double *wt_val, int32_t *wt_len, void *ws,
                                          size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_rowptr && cur && end && alpha && beta && wt_ptr && wt_len &&
+  LG_REQUIRE(item_rowptr && inv_deg && cur && count && alpha && beta && wt_ptr && wt_len &&
                  n_items >= 0,
              "lg_spread_tile_weight_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && item_begin >= 0,
@@ -612,13 +668,13 @@ extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32
     return LG_ERR_HIP;
   }
   const unsigned rb = (unsigned)((n_items + 3) / 4);
-  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_rowptr,
-                                               user_items, n_items, cur, end, alpha, beta,
-                                               wt_ptr, wt_col, wt_val, wt_len);
+  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_items, inv_deg,
+                                               n_items, cur, count, alpha, beta, wt_ptr,
+                                               wt_col, wt_val, wt_len);
   k_hub_list<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
       wt_ptr, n_items, (unsigned long long *)n_hub, hub_rows);
   k_tile_weight_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
-      hub_rows, n_hub, item_rowptr, item_users, user_rowptr, user_items, cur, end, alpha, beta,
+      hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, alpha, beta,
       item_begin, tile, wt_ptr, wt_col, wt_val, wt_len);
   return launch_status("lg_spread_tile_weight_f64");
 }
@@ -637,7 +693,7 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
   // 4 waves per block, tile doubles of LDS per wave (<= 64 KiB per wave at tile 8192)
   const int waves = tile <= 2048 ? 4 : (tile <= 4096 ? 2 : 1);
   const size_t lds = (size_t)waves * tile * sizeof(double);
-  k_tile_resource<8><<<dim3((unsigned)((n_users + waves - 1) / waves)), dim3(64 * waves), lds,
+  k_tile_resource<16><<<dim3((unsigned)((n_users + waves - 1) / waves)), dim3(64 * waves), lds,
                        (hipStream_t)stream>>>(user_rowptr, user_items, n_users, wt_ptr, wt_len,
                                               wt_col, wt_val, item_begin, tile, F, ldf);
   return launch_status("lg_spread_tile_resource_f64");

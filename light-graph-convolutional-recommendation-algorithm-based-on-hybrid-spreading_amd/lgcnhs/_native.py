@@ -64,8 +64,9 @@ SIGNATURES = {
         [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
     ),
     "lg_hybrid_factors_f64": (ctypes.c_int, [_vp, _i64, _f64, _vp, _vp, _vp]),
-    "lg_spread_tile_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
-    "lg_spread_tile_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "lg_inv_degree_f64": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
+    "lg_spread_tile_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "lg_spread_tile_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "lg_spread_tile_weight_ws_bytes": (_sz, [_i64]),
     "lg_spread_tile_weight_f64": (
         ctypes.c_int,

@@ -324,6 +324,11 @@ class TileWeights:
         I = A.n_items
         self.cur = A.by_user.rowptr[:-1].contiguous().clone()
         self.end = torch.empty_like(self.cur)
+        self.count = torch.empty(A.n_users, dtype=torch.uint16, device=dev)
+        self.inv_deg = torch.empty(A.n_users, dtype=torch.float64, device=dev)
+        N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,
+                                          N.ptr(self.inv_deg), N.stream_handle(dev)),
+                "lg_inv_degree_f64")
         self.bound = torch.empty(I, dtype=torch.int64, device=dev)
         self.ptr = torch.zeros(I + 1, dtype=torch.int64, device=dev)
         self.len = torch.empty(I, dtype=torch.int32, device=dev)
@@ -347,10 +352,11 @@ class TileWeights:
         width = min(self.tile, I - j0)
         N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
                                         A.n_users, j0 + width, N.ptr(self.cur),
-                                        N.ptr(self.end), strm), "lg_spread_tile_cursor")
+                                        N.ptr(self.end), N.ptr(self.count), strm),
+                "lg_spread_tile_cursor")
         N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
-                                       N.ptr(self.cur), N.ptr(self.end), N.ptr(self.bound),
-                                       strm), "lg_spread_tile_bound")
+                                       N.ptr(self.count), N.ptr(self.bound), strm),
+                "lg_spread_tile_bound")
         torch.cumsum(self.bound, 0, out=self.ptr[1:])
         total = int(self.ptr[-1])  # host sync: sizes the row storage
         if total > self.col.numel():
@@ -358,8 +364,8 @@ class TileWeights:
             self.col = torch.empty(cap, dtype=torch.int32, device=self.dev)
             self.val = torch.empty(cap, dtype=torch.float64, device=self.dev)
         N.check(L.lg_spread_tile_weight_f64(
-            N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.rowptr),
-            N.ptr(A.by_user.col), I, N.ptr(self.cur), N.ptr(self.end), N.ptr(self.alpha),
+            N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
+            N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count), N.ptr(self.alpha),
             N.ptr(self.beta), j0, self.tile, N.ptr(self.ptr), N.ptr(self.col),
             N.ptr(self.val), N.ptr(self.len), N.ptr(self.ws), self.ws.numel(), strm),
             "lg_spread_tile_weight_f64")
@@ -394,11 +400,15 @@ def tile_topk(F: torch.Tensor, j0: int, n_cols: int, k: int, vals: torch.Tensor,
 def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       drop: bool = True, eu: torch.Tensor | None = None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
-                      tile: int = 2048, block_users: int | None = None):
+                      tile: int = 2048, scratch_bytes: int = 4 << 30):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). Bitwise the result of
     spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
-    ``users`` restricts the output to a row range (the multi-GPU shard)."""
+
+    Each tile of W (user-independent) is built once and applied to all the users; the F
+    columns of consecutive tiles are collected in a [users, span] scratch (span = as many
+    whole tiles as ``scratch_bytes`` allows) and merged into the running top-k lists once
+    per span. ``users`` restricts the output to a row range (the multi-GPU shard)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     n = u1 - u0
     dev = A.k_item.device
@@ -406,17 +416,17 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     idxs = torch.full((n, k), -1, dtype=torch.int64, device=dev)
     if n == 0 or A.n_items == 0:
         return vals, idxs
-    if block_users is None:
-        block_users = max(1, min(n, (1 << 30) // (tile * 8)))  # ~1 GiB of F per block
-    F = torch.empty((min(block_users, n), tile), dtype=torch.float64, device=dev)
+    tile = min(int(tile), A.n_items)
+    span = max(tile, scratch_bytes // (n * 8) // tile * tile)
+    span = min(span, -(-A.n_items // tile) * tile)
+    F = torch.empty((n, span), dtype=torch.float64, device=dev)
     tw = TileWeights(A, lam, tile)
     ex = excl.slice_rows(u0, u1) if excl is not None else None
-    for j0 in range(0, A.n_items, tile):
-        tw.build(j0)
-        for b0 in range(0, n, block_users):
-            b1 = min(n, b0 + block_users)
-            Fb = tw.resource(u0 + b0, u0 + b1, F[: b1 - b0])
-            tile_topk(Fb, j0, tw.width, k, vals[b0:b1], idxs[b0:b1], j0 == 0,
-                      ex.slice_rows(b0, b1) if ex is not None else None, drop,
-                      None if eu is None else eu[u0 + b0:u0 + b1], ei)
+    eu_r = None if eu is None else eu[u0:u1]
+    for s0 in range(0, A.n_items, span):
+        s1 = min(A.n_items, s0 + span)
+        for j0 in range(s0, s1, tile):
+            tw.build(j0)
+            tw.resource(u0, u1, F[:, j0 - s0:])
+        tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == 0, ex, drop, eu_r, ei)
     return vals, idxs

@@ -74,10 +74,12 @@ def test_spread_topk_tiled_equals_dense(k, tile, mode):
     W = ops.hybrid_weight(ops.spread_general(A), A.k_item, lam)
     kw = dict(eu=eu if use_g else None, ei=ei if use_g else None)
     v0, i0 = ops.spread_topk(A, W, k, A.by_user, drop=drop, **kw)
-    v1, i1 = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile,
-                                   block_users=128, **kw)
-    assert torch.equal(i1, i0)
-    assert torch.equal(v1.view(torch.int64), v0.view(torch.int64))
+    # scratch for one tile (span = tile) and for several tiles per top-k merge
+    for scratch in (1, 3 * U * 8 * tile):
+        v1, i1 = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile,
+                                       scratch_bytes=scratch, **kw)
+        assert torch.equal(i1, i0)
+        assert torch.equal(v1.view(torch.int64), v0.view(torch.int64))
 
 
 def test_spread_topk_tiled_user_shards():
