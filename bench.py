@@ -175,6 +175,67 @@ def bench_small_config(dev, k):
     return res
 
 
+def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, users_per_rank, lam=0.5,
+                 tile=2048):
+    """C5-shape LGCNHS recommendation (SpreadLightGCN, model/SpreadLightGCN/model.py:107-153 +
+    recommend.py:18-52): per user, top-k of G * F with F = A @ HybridS(A, general_W, lam)
+    and G the fp32 e0 score, train|val items dropped; the factored tile path
+    (ops.spread_topk_tiled), users sharded over the ranks with no exchange. Timed end to
+    end: every W tile is built once per rank (user-independent) and applied to the rank's
+    users. Also the Douban-shaped dense path (configs[2]: SpreadLightGCNOpti, lam=0.5)."""
+    from lgcnhs import ops
+    from lgcnhs.synth import synth_interactions
+    A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
+    n = min(users_per_rank, -(-U // world))
+    u0 = min(rank * n, U - n)
+    eu = e0_orig[:U]
+    ei = e0_orig[U:U + I].contiguous()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    _, idx = ops.spread_topk_tiled(A, lam, k, A.by_user, True, eu, ei, users=slice(u0, u0 + n),
+                                   tile=tile)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    filled = float((idx >= 0).float().mean().item())
+    del A, idx
+    torch.cuda.empty_cache()
+    res = {"recs_per_s": n * world / dt, "users_per_rank": n, "seconds": dt, "k": k,
+           "lambda": lam, "tile": tile, "filled_frac": filled,
+           "path": "lg_spread_tile_{cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 (G by f32 MFMA)"}
+    if world == 1:
+        # configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), dense
+        # general_W / W (fp64 I x I), fused G * F top-k
+        du, di, de = 600, 20_000, 60_000
+        users, items = synth_interactions(du, di, de, seed=3, dist="zipf")
+        g = torch.Generator(device=dev).manual_seed(42)
+        deu = torch.randn(du, 64, device=dev, generator=g) * 0.1
+        dei = torch.randn(di, 64, device=dev, generator=g) * 0.1
+
+        def dense():
+            Ad = ops.Interactions.from_pairs(torch.as_tensor(users), torch.as_tensor(items), du,
+                                             di, dev)
+            W = ops.hybrid_weight(ops.spread_general(Ad), Ad.k_item, lam)
+            return ops.spread_topk(Ad, W, k, Ad.by_user, True, deu, dei)
+        dense()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dense()
+        torch.cuda.synchronize()
+        dd = time.perf_counter() - t0
+        res["c3_douban_shape"] = {"users": du, "items": di, "interactions": de, "seconds": dd,
+                                  "recs_per_s": du / dd,
+                                  "path": "lg_spread_general_f64 + lg_hybrid_weight_f64 + "
+                                          "lg_spread_resource_f64 + lg_rows_topk_f64"}
+        torch.cuda.empty_cache()
+    return res
+
+
 def load_traffic(workload, world):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -195,6 +256,9 @@ def main():
     ap.add_argument("--k", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-topk", action="store_true")
+    ap.add_argument("--no-spread", action="store_true")
+    ap.add_argument("--spread-users", type=int, default=131072,
+                    help="users per rank for the LGCNHS spreading phase")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
@@ -303,6 +367,14 @@ def main():
                 "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
                 "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
 
+    spread = None
+    if not args.no_spread:
+        try:
+            spread = bench_spread(keys, U, I, e0_orig, args.k, rank, world, dev,
+                                  args.spread_users)
+        except Exception as ex:  # a side measurement never hides the main result
+            log(f"spread bench failed: {ex!r}")
+
     small = None
     if world == 1 and not args.no_small:
         try:
@@ -333,6 +405,7 @@ def main():
                          "avg_launch_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes},
             "topk": topk,
+            "spread": spread,
             "other_dims": extra,
             "c2_ml1m_shape": small,
             "cpu_baseline": cpu,

@@ -10,6 +10,7 @@ rows_topk        argsort + filter + [:k], G * F    model/SpreadMethod/recommend.
                                                    model/SpreadLightGCN/model.py:151
 spread_topk_tiled  the above over item tiles,      (same; for catalogs whose I x I W
                    never holding an I x I matrix    does not fit)
+spread_recommend   dense or tiled, whichever fits  model/SpreadMethod/recommend.py:59-115
 """
 from __future__ import annotations
 
@@ -430,3 +431,28 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
             tw.resource(u0, u1, F[:, j0 - s0:])
         tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == 0, ex, drop, eu_r, ei)
     return vals, idxs
+
+
+def dense_spread_fits(n_items: int, device, fraction: float = 0.25) -> bool:
+    """True when general_W and W (two fp64 I x I matrices) fit in ``fraction`` of the free
+    device memory: the dense path; otherwise the factored tile path."""
+    free, _ = torch.cuda.mem_get_info(device)
+    return 2 * 8 * n_items * n_items <= fraction * free
+
+
+def spread_recommend(A: Interactions, lam: float, k: int, excl: RowSets | None,
+                     drop: bool = True, eu: torch.Tensor | None = None,
+                     ei: torch.Tensor | None = None, transpose: bool = False,
+                     tiled: bool | None = None):
+    """Per-user top-k of (G *) A @ HybridS(A, general_W(^T), lam), dense (I x I matrices on
+    the device) or factored over item tiles (tiled=None: dense when it fits). The two
+    paths give the same bits. general_W is exactly symmetric (entry (i, j) and (j, i) are
+    the same sum, over the common users ascending, of the same fl(1/k_v)), so the
+    reference's general_W.T overrides (model/SpreadMethod/recommend.py:89-91, :99-101)
+    are served by either path unchanged."""
+    if tiled is None:
+        tiled = not dense_spread_fits(A.n_items, A.k_item.device)
+    if tiled:
+        return spread_topk_tiled(A, lam, k, excl, drop, eu, ei)
+    W = hybrid_weight(spread_general(A), A.k_item, lam, transpose)
+    return spread_topk(A, W, k, excl, drop, eu, ei)

@@ -43,17 +43,19 @@ def recommendForAllUser(F_new: np.ndarray, user_num: int, train_data_df: pd.Data
 
 
 def spread_lightgcn_topk(model, user_num: int, item_num: int, train_data_df: pd.DataFrame,
-                         val_data_df: pd.DataFrame, lambda_val: float, k: int, device=None):
+                         val_data_df: pd.DataFrame, lambda_val: float, k: int, device=None,
+                         tiled: bool | None = None):
     """Device (values fp64, items int64) of the whole LGCNHS recommendation."""
     dev = device or gpu_device(model.users_emb.weight)
     both = pd.concat([train_data_df, val_data_df])
     inter = ops.Interactions.from_pairs(
         torch.from_numpy(both["user_id"].to_numpy(np.int64)),
         torch.from_numpy(both["item_id"].to_numpy(np.int64)), user_num, item_num, dev)
-    W = ops.hybrid_weight(ops.spread_general(inter), inter.k_item, lambda_val)
     eu = model.users_emb.weight.detach().to(dev, torch.float32).contiguous()
     ei = model.items_emb.weight.detach().to(dev, torch.float32).contiguous()
-    return ops.spread_topk(inter, W, k, inter.by_user, drop=True, eu=eu, ei=ei)
+    # dense I x I general_W / W when they fit, else the factored tile path (same bits)
+    return ops.spread_recommend(inter, lambda_val, k, inter.by_user, drop=True, eu=eu, ei=ei,
+                                tiled=tiled)
 
 
 def recommendSpreadLightGCN(user_num: int, item_num: int, rating_df: pd.DataFrame,

@@ -50,23 +50,23 @@ def recommendForAllUser(F_new: np.ndarray, user_num: int, train_data_df: pd.Data
 
 def spread_method_topk(user_num: int, item_num: int, train_data_df: pd.DataFrame,
                        val_data_df: pd.DataFrame, method: str, lambda_val: float,
-                       dataset: str, k: int, unfiltered: bool = False, device=None):
+                       dataset: str, k: int, unfiltered: bool = False, device=None,
+                       tiled: bool | None = None):
     """Device (values, items) of the whole spreading recommendation."""
     dev = device or gpu_device()
     both = pd.concat([train_data_df, val_data_df])
     inter = ops.Interactions.from_pairs(
         torch.from_numpy(both["user_id"].to_numpy(np.int64)),
         torch.from_numpy(both["item_id"].to_numpy(np.int64)), user_num, item_num, dev)
-    gW = ops.spread_general(inter)
     transpose = False
     if method == "ProbS" and dataset == "movielens":  # reference :87-91
         lambda_val, transpose = 0.01, True
     elif method == "HeatS" and dataset == "douban":  # reference :97-101
         lambda_val, transpose = 0.99, True
-    W = ops.hybrid_weight(gW, inter.k_item, lambda_val, transpose)
-    del gW
     excl = inter.by_user  # train|val positives == the nonzeros of A
-    return ops.spread_topk(inter, W, k, excl, drop=not unfiltered)
+    # dense I x I general_W / W when they fit, else the factored tile path (same bits)
+    return ops.spread_recommend(inter, lambda_val, k, excl, drop=not unfiltered,
+                                transpose=transpose, tiled=tiled)
 
 
 def recommendSpreadMethod(user_num: int, item_num: int, train_data_df: pd.DataFrame,

@@ -124,3 +124,28 @@ def test_tile_api_errors():
     tw.build(0)
     with pytest.raises(ValueError):
         tw.build(48)  # not the next tile
+
+
+@pytest.mark.parametrize("zipf", [False, True])
+def test_general_w_exactly_symmetric(zipf):
+    """general_W[i][j] and [j][i] are the same sum (common users ascending, fl(1/k_v)), so
+    the reference's general_W.T overrides need no transposed tile path."""
+    from lgcnhs import ops
+    A = _inter(400, 600, 20000 if zipf else 8000, seed=9, zipf=zipf)
+    gW = ops.spread_general(A)
+    assert torch.equal(gW.view(torch.int64), gW.t().contiguous().view(torch.int64))
+
+
+@pytest.mark.parametrize("method,dataset", [("ProbS", "movielens"), ("HeatS", "douban"),
+                                            ("HybridS", "douban"), ("ProbS", "douban")])
+def test_spread_method_tiled_dispatch_equals_dense(method, dataset):
+    """spread_method_topk through the tile path (forced) = the dense path bit for bit,
+    including the lambda / general_W.T overrides and the unfiltered ML-ProbS branch."""
+    from lgcnhs.synth import synth_dataframes
+    from model.SpreadMethod.recommend import spread_method_topk
+    _, tr, va, _ = synth_dataframes(150, 400, 6000, seed=7, dist="zipf")
+    unf = method == "ProbS" and dataset == "movielens"
+    out = [spread_method_topk(150, 400, tr, va, method, 0.35, dataset, 15, unfiltered=unf,
+                              tiled=t) for t in (False, True)]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))
