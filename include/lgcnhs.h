@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 4
+#define LG_ABI_VERSION 5
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -230,28 +230,29 @@ int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
 /* Row i of W restricted to the tile, for every item i:
  *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} inv_deg[v])
  *             / (alpha[i] * beta[j])          (den == 0 -> 1)
- * written at wt_col/wt_val[wt_ptr[i] .. wt_ptr[i] + wt_len[i]) in ascending j, where
- * wt_ptr[n_items + 1] is the exclusive prefix of lg_spread_tile_bound's bounds (row
- * capacities); cur/count from lg_spread_tile_cursor, inv_deg from lg_inv_degree_f64 over
- * the user rows. ws: lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in
- * [1, 8192]; every item of the tile must lie in [item_begin, item_begin + tile). */
+ * written in ascending j as 12-byte entries {int32 j; fp64 value, 4-byte aligned} at
+ * wt_ent[wt_ptr[i] .. wt_ptr[i] + len_i), where wt_ptr[n_items + 1] is the exclusive prefix
+ * of lg_spread_tile_bound's bounds (row capacities), and wt_meta[i] = wt_ptr[i] |
+ * (len_i << 48) (one 8-byte lookup per row for the resource pass); cur/count from
+ * lg_spread_tile_cursor, inv_deg from lg_inv_degree_f64 over the user rows. ws:
+ * lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in [1, 8192]; every item
+ * of the tile must lie in [item_begin, item_begin + tile). */
 size_t lg_spread_tile_weight_ws_bytes(int64_t n_items);
 int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
                               const int32_t *user_items, const double *inv_deg,
                               int64_t n_items, const int64_t *cur, const uint16_t *count,
                               const double *alpha, const double *beta, int32_t item_begin,
-                              int32_t tile, const int64_t *wt_ptr, int32_t *wt_col,
-                              double *wt_val, int32_t *wt_len, void *ws, size_t ws_bytes,
+                              int32_t tile, const int64_t *wt_ptr, void *wt_ent,
+                              uint64_t *wt_meta, void *ws, size_t ws_bytes,
                               lg_stream_t stream);
 
 /* F[u][j - item_begin] = sum_{i in items(u), ascending} W[i][j] for the n_users rows of
  * user_rowptr (pass user_rowptr + u0 for a block) and j in [item_begin, item_begin + tile);
- * F row-major with leading dim ldf >= tile. */
+ * F row-major with leading dim ldf >= tile; wt_meta / wt_ent from lg_spread_tile_weight_f64. */
 int lg_spread_tile_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                int64_t n_users, const int64_t *wt_ptr,
-                                const int32_t *wt_len, const int32_t *wt_col,
-                                const double *wt_val, int32_t item_begin, int32_t tile,
-                                double *F, int64_t ldf, lg_stream_t stream);
+                                int64_t n_users, const uint64_t *wt_meta, const void *wt_ent,
+                                int32_t item_begin, int32_t tile, double *F, int64_t ldf,
+                                lg_stream_t stream);
 
 /* Merge columns [item_begin, item_begin + n_cols) of (G *) F (F[r][0..n_cols), leading dim
  * ldf; G as in lg_rows_topk_f64 with eu = the rows' user embeddings and ei = all item

@@ -34,6 +34,22 @@ namespace lg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// One entry of a W tile row: 12 bytes, {item, fp64 value as two dwords} (4-byte aligned, so
+// a row of n entries is 12n contiguous bytes: fewer 128-B lines per random row than split
+// column / value arrays). meta[i] = (row start) | (row length << 48).
+struct WEnt {
+  int32_t col;
+  uint32_t lo, hi;
+};
+constexpr int kMetaShift = 48;
+constexpr uint64_t kMetaPtrMask = (1ull << kMetaShift) - 1;
+
+__device__ __forceinline__ void put_ent(WEnt *__restrict__ ent, int64_t pos, int32_t col,
+                                        double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  ent[pos] = WEnt{col, (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
 __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
                                                         int64_t n, double lambda,
                                                         double *__restrict__ alpha,
@@ -94,8 +110,7 @@ template <int M>
 __device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, const double *sw, int n,
                                                int64_t wbase, double alpha_i,
                                                const double *__restrict__ beta,
-                                               int32_t *__restrict__ wt_col,
-                                               double *__restrict__ wt_val) {
+                                               WEnt *__restrict__ wt_ent) {
   const int lane = lane_id();
   int k[M], id[M];
 #pragma unroll
@@ -128,8 +143,7 @@ __device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, const double
       double den = alpha_i * beta[item];
       if (den == 0.0) den = 1.0;
       const int pos = base + __popcll(hb & lanemask_lt());
-      wt_col[wbase + pos] = item;
-      wt_val[wbase + pos] = s / den;
+      put_ent(wt_ent, wbase + pos, item, s / den);
     }
     base += __popcll(hb);
   }
@@ -142,8 +156,8 @@ __global__ __launch_bounds__(256) void k_tile_weight(
     const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
     int64_t n_items, const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
     const double *__restrict__ alpha, const double *__restrict__ beta,
-    const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
-    double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
+    const int64_t *__restrict__ wt_ptr, WEnt *__restrict__ wt_ent,
+    uint64_t *__restrict__ wt_meta) {
   __shared__ int skey[4][kSortMax];
   __shared__ int sid[4][kSortMax];
   __shared__ double sw[4][kSortMax];
@@ -154,7 +168,7 @@ __global__ __launch_bounds__(256) void k_tile_weight(
   const int64_t wbase = wt_ptr[i];
   const int64_t bound = wt_ptr[i + 1] - wbase;
   if (bound == 0) {
-    if (lane == 0) wt_len[i] = 0;
+    if (lane == 0) wt_meta[i] = (uint64_t)wbase;
     return;
   }
   if (bound > kSortMax) return;  // hub row: k_tile_weight_hub
@@ -193,14 +207,14 @@ __global__ __launch_bounds__(256) void k_tile_weight(
   int len;
   if (n <= 64)
     len = sort_reduce_row<1>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_col, wt_val);
+                             wt_ent);
   else if (n <= 128)
     len = sort_reduce_row<2>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_col, wt_val);
+                             wt_ent);
   else
     len = sort_reduce_row<4>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_col, wt_val);
-  if (lane == 0) wt_len[i] = len;
+                             wt_ent);
+  if (lane == 0) wt_meta[i] = (uint64_t)wbase | ((uint64_t)len << kMetaShift);
 }
 
 // Hub rows (> kSortMax pairs): one 256-thread block per row (grid-stride over the hub list),
@@ -212,8 +226,8 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
     const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
     const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
     const double *__restrict__ alpha, const double *__restrict__ beta, int32_t item_begin,
-    int32_t tile, const int64_t *__restrict__ wt_ptr, int32_t *__restrict__ wt_col,
-    double *__restrict__ wt_val, int32_t *__restrict__ wt_len) {
+    int32_t tile, const int64_t *__restrict__ wt_ptr, WEnt *__restrict__ wt_ent,
+    uint64_t *__restrict__ wt_meta) {
   extern __shared__ double acc[];  // tile doubles
   __shared__ int wsum[4];
   const int64_t nh = *n_hub;
@@ -251,13 +265,12 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
         double den = a * beta[item];
         if (den == 0.0) den = 1.0;
         const int pos = base + before_w + __popcll(b & lanemask_lt());
-        wt_col[wbase + pos] = item;
-        wt_val[wbase + pos] = acc[j] / den;
+        put_ent(wt_ent, wbase + pos, item, acc[j] / den);
       }
       base += total;
       __syncthreads();
     }
-    if (threadIdx.x == 0) wt_len[i] = base;
+    if (threadIdx.x == 0) wt_meta[i] = (uint64_t)wbase | ((uint64_t)base << kMetaShift);
     __syncthreads();
   }
 }
@@ -271,60 +284,88 @@ __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ wt
   if (wt_ptr[i + 1] - wt_ptr[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
 }
 
-// F[u][j - j0] = sum over items(u) ascending of W[i][j]; one wave per user, RB rows in
-// flight. LDS: tile doubles per wave (dynamic).
-template <int RB>
+// F[u][j - j0] = sum over items(u) ascending of W[i][j]; one wave per user, the tile's
+// accumulator in LDS (tile doubles per wave) plus a 128-row index (LDS, 1.5 KiB per wave).
+// Rows are taken 128 at a time: their metadata is fetched in one round trip (two loads per
+// lane), then their entries are flattened: lane l takes entries e = e0 + q*64 + l of the
+// concatenated rows (its row found by a binary search over the rows' inclusive length
+// prefix in LDS), so each load instruction moves 64 useful 12-byte entries whatever the row
+// lengths, UF of them in flight per lane. Entries go in with ds_add_f64; entries of one
+// instruction that hit the same column come from rows in lane order, and rows are
+// flattened in ascending order, so each column still receives its rows' values in
+// ascending row order (the order of lg_spread_resource_f64).
+constexpr int kResRows = 128;
+constexpr int kResIdxBytes = kResRows * (4 + 8);
+
+template <int UF>
 __global__ __launch_bounds__(256) void k_tile_resource(
     const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_users, const int64_t *__restrict__ wt_ptr, const int32_t *__restrict__ wt_len,
-    const int32_t *__restrict__ wt_col, const double *__restrict__ wt_val, int32_t item_begin,
-    int32_t tile, double *__restrict__ F, int64_t ldf) {
+    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
+    int32_t item_begin, int32_t tile, double *__restrict__ F, int64_t ldf) {
   extern __shared__ double lds[];
   const int wave = threadIdx.x / 64;
+  const int wpb = blockDim.x / 64;
   const int lane = lane_id();
-  const int64_t u = (int64_t)blockIdx.x * (blockDim.x / 64) + wave;
+  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
   if (u >= n_users) return;
   double *acc = lds + (int64_t)wave * tile;
+  char *idx = reinterpret_cast<char *>(lds + (int64_t)wpb * tile) + wave * kResIdxBytes;
+  int64_t *s_base = reinterpret_cast<int64_t *>(idx);               // entry e of row r: base_r + e
+  int *s_incl = reinterpret_cast<int *>(idx + kResRows * 8);         // inclusive entry prefix
   for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
-  wave_sync();
   const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
-  for (int64_t p0 = pb; p0 < pe; p0 += 64) {
-    // lane l: metadata of row p0 + l
-    int64_t rp = 0;
-    int rl = 0;
-    if (p0 + lane < pe) {
-      const int32_t i = user_items[p0 + lane];
-      rp = wt_ptr[i];
-      rl = wt_len[i];
+  for (int64_t p0 = pb; p0 < pe; p0 += kResRows) {
+    uint64_t m0 = 0, m1 = 0;
+    {
+      const int32_t i0 = p0 + lane < pe ? user_items[p0 + lane] : -1;
+      const int32_t i1 = p0 + 64 + lane < pe ? user_items[p0 + 64 + lane] : -1;
+      if (i0 >= 0) m0 = wt_meta[i0];
+      if (i1 >= 0) m1 = wt_meta[i1];
     }
-    const int nr = (pe - p0) < 64 ? (int)(pe - p0) : 64;
-    for (int r0 = 0; r0 < nr; r0 += RB) {
-      // RB rows' first 64 entries in flight together
-      int col[RB];
-      double val[RB];
-      int len[RB];
-      int64_t ptr[RB];
+    const int rl0 = (int)(m0 >> kMetaShift), rl1 = (int)(m1 >> kMetaShift);
+    int in0 = rl0, in1 = rl1;
 #pragma unroll
-      for (int q = 0; q < RB; ++q) {
-        const int r = r0 + q;
-        len[q] = r < nr ? __shfl(rl, r) : 0;
-        ptr[q] = __shfl(rp, r < nr ? r : 0);
-        col[q] = 0;
-        val[q] = 0.0;
-        if (lane < len[q]) {
-          col[q] = wt_col[ptr[q] + lane];
-          val[q] = wt_val[ptr[q] + lane];
-        }
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y0 = __shfl_up(in0, o), y1 = __shfl_up(in1, o);
+      if (lane >= o) { in0 += y0; in1 += y1; }
+    }
+    const int t0 = __shfl(in0, 63);
+    in1 += t0;
+    const int total = __shfl(in1, 63);
+    wave_sync();  // the previous group's readers of the index are done
+    s_incl[lane] = in0;
+    s_incl[64 + lane] = in1;
+    s_base[lane] = (int64_t)(m0 & kMetaPtrMask) - (in0 - rl0);
+    s_base[64 + lane] = (int64_t)(m1 & kMetaPtrMask) - (in1 - rl1);
+    wave_sync();
+    for (int e0 = 0; e0 < total; e0 += 64 * UF) {
+      // r[q] = number of rows whose inclusive end is <= e[q] (the row holding entry e[q]):
+      // the UF binary searches advance in lockstep (independent LDS reads per step, no
+      // branch), then the UF entry loads issue back to back. Lanes past the end re-read
+      // the last entry and skip the add.
+      int e[UF], r[UF];
+#pragma unroll
+      for (int q = 0; q < UF; ++q) {
+        const int x = e0 + q * 64 + lane;
+        e[q] = x < total ? x : total - 1;
+        r[q] = 0;
       }
 #pragma unroll
-      for (int q = 0; q < RB; ++q) {
-        if (lane < len[q]) acc[col[q] - item_begin] += val[q];
-        for (int e = 64 + lane; e < len[q]; e += 64)  // long rows: rest of the entries
-          acc[wt_col[ptr[q] + e] - item_begin] += wt_val[ptr[q] + e];
-        wave_sync();  // the next row may hit the same columns from other lanes
-      }
+      for (int st = 64; st > 0; st >>= 1)
+#pragma unroll
+        for (int q = 0; q < UF; ++q) r[q] += s_incl[r[q] + st - 1] <= e[q] ? st : 0;
+      WEnt w[UF];
+#pragma unroll
+      for (int q = 0; q < UF; ++q) w[q] = wt_ent[s_base[r[q]] + e[q]];
+#pragma unroll
+      for (int q = 0; q < UF; ++q)
+        if (e0 + q * 64 + lane < total)
+          __hip_atomic_fetch_add(&acc[w[q].col - item_begin],
+                                 __hiloint2double((int)w[q].hi, (int)w[q].lo),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  wave_sync();
   double *row = F + u * ldf;
   for (int j = lane; j < tile; j += 64) row[j] = acc[j];
 }
@@ -539,16 +580,27 @@ __global__ __launch_bounds__(128) void k_tile_topk(
     }
   };
 
-  float afA[Q], afB[Q];
-  double fA[NG][4], fB[NG][4];
-  load_step(0, afA, fA);
-  for (int it = 0;; it += 32) {
-    load_step(it + 16, afB, fB);  // clamped: harmless past the end
-    process(it, afA, fA);
+  // ring of 4 register buffers: the loads of step t+3 are in flight while step t is
+  // processed (F comes from HBM and is not shared between waves, so the wave needs its
+  // own memory-level parallelism); past the end the loads are clamped and harmless
+  float af0[Q], af1[Q], af2[Q], af3[Q];
+  double f0[NG][4], f1[NG][4], f2[NG][4], f3[NG][4];
+  load_step(0, af0, f0);
+  load_step(16, af1, f1);
+  load_step(32, af2, f2);
+  for (int it = 0;; it += 64) {
+    load_step(it + 48, af3, f3);
+    process(it, af0, f0);
     if (it + 16 >= n_cols) break;
-    load_step(it + 32, afA, fA);
-    process(it + 16, afB, fB);
+    load_step(it + 64, af0, f0);
+    process(it + 16, af1, f1);
     if (it + 32 >= n_cols) break;
+    load_step(it + 80, af1, f1);
+    process(it + 32, af2, f2);
+    if (it + 48 >= n_cols) break;
+    load_step(it + 96, af2, f2);
+    process(it + 48, af3, f3);
+    if (it + 64 >= n_cols) break;
   }
 
   wave_sync();
@@ -646,10 +698,9 @@ extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32
                                          int64_t n_items, const int64_t *cur,
                                          const uint16_t *count, const double *alpha,
                                          const double *beta, int32_t item_begin, int32_t tile,
-                                         const int64_t *wt_ptr, int32_t *wt_col,
-                                         double *wt_val, int32_t *wt_len, void *ws,
-                                         size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && inv_deg && cur && count && alpha && beta && wt_ptr && wt_len &&
+                                         const int64_t *wt_ptr, void *wt_ent, uint64_t *wt_meta,
+                                         void *ws, size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && inv_deg && cur && count && alpha && beta && wt_ptr && wt_meta &&
                  n_items >= 0,
              "lg_spread_tile_weight_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && item_begin >= 0,
@@ -670,32 +721,32 @@ extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32
   const unsigned rb = (unsigned)((n_items + 3) / 4);
   k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_items, inv_deg,
                                                n_items, cur, count, alpha, beta, wt_ptr,
-                                               wt_col, wt_val, wt_len);
+                                               (WEnt *)wt_ent, wt_meta);
   k_hub_list<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
       wt_ptr, n_items, (unsigned long long *)n_hub, hub_rows);
   k_tile_weight_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
       hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, alpha, beta,
-      item_begin, tile, wt_ptr, wt_col, wt_val, wt_len);
+      item_begin, tile, wt_ptr, (WEnt *)wt_ent, wt_meta);
   return launch_status("lg_spread_tile_weight_f64");
 }
 
 extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
                                            const int32_t *user_items, int64_t n_users,
-                                           const int64_t *wt_ptr, const int32_t *wt_len,
-                                           const int32_t *wt_col, const double *wt_val,
+                                           const uint64_t *wt_meta, const void *wt_ent,
                                            int32_t item_begin, int32_t tile, double *F,
                                            int64_t ldf, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && wt_ptr && wt_len && F && n_users >= 0 && ldf >= tile,
+  LG_REQUIRE(user_rowptr && wt_meta && F && n_users >= 0 && ldf >= tile,
              "lg_spread_tile_resource_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192, "lg_spread_tile_resource_f64: tile %d not in [1, 8192]",
              tile);
   if (n_users == 0) return LG_OK;
-  // 4 waves per block, tile doubles of LDS per wave (<= 64 KiB per wave at tile 8192)
-  const int waves = tile <= 2048 ? 4 : (tile <= 4096 ? 2 : 1);
-  const size_t lds = (size_t)waves * tile * sizeof(double);
+  // tile doubles of LDS per wave (<= 64 KiB at tile 8192); small blocks so the CU's LDS
+  // holds as many waves as it can
+  const int waves = tile <= 1024 ? 4 : (tile <= 2048 ? 2 : 1);
+  const size_t lds = (size_t)waves * (tile * sizeof(double) + kResIdxBytes);
   k_tile_resource<16><<<dim3((unsigned)((n_users + waves - 1) / waves)), dim3(64 * waves), lds,
-                       (hipStream_t)stream>>>(user_rowptr, user_items, n_users, wt_ptr, wt_len,
-                                              wt_col, wt_val, item_begin, tile, F, ldf);
+                       (hipStream_t)stream>>>(user_rowptr, user_items, n_users, wt_meta,
+                                              (const WEnt *)wt_ent, item_begin, tile, F, ldf);
   return launch_status("lg_spread_tile_resource_f64");
 }
 

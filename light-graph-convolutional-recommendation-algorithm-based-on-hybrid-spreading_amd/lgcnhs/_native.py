@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "liblgcnhs.so")
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -70,12 +70,12 @@ SIGNATURES = {
     "lg_spread_tile_weight_ws_bytes": (_sz, [_i64]),
     "lg_spread_tile_weight_f64": (
         ctypes.c_int,
-        [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
-         _sz, _vp],
+        [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _sz,
+         _vp],
     ),
     "lg_spread_tile_resource_f64": (
         ctypes.c_int,
-        [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp],
+        [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp],
     ),
     "lg_tile_topk_f64": (
         ctypes.c_int,

@@ -332,13 +332,27 @@ class TileWeights:
                 "lg_inv_degree_f64")
         self.bound = torch.empty(I, dtype=torch.int64, device=dev)
         self.ptr = torch.zeros(I + 1, dtype=torch.int64, device=dev)
-        self.len = torch.empty(I, dtype=torch.int32, device=dev)
+        self.meta = torch.empty(I, dtype=torch.int64, device=dev)  # ptr | len << 48
         self.ws = torch.empty(max(1, N.lib().lg_spread_tile_weight_ws_bytes(I)),
                               dtype=torch.uint8, device=dev)
-        self.col = torch.empty(0, dtype=torch.int32, device=dev)
-        self.val = torch.empty(0, dtype=torch.float64, device=dev)
+        self.ent = torch.empty(0, dtype=torch.int32, device=dev)  # 3 int32 per entry
         self.j0 = None
         self.width = 0
+
+    @property
+    def len(self) -> torch.Tensor:
+        """Entries of each W row in the current tile."""
+        return (self.meta >> 48).to(torch.int32)
+
+    @property
+    def col(self) -> torch.Tensor:
+        """Item of each entry slot (row i's entries at ptr[i] .. ptr[i] + len[i])."""
+        return self.ent.view(-1, 3)[:, 0]
+
+    @property
+    def val(self) -> torch.Tensor:
+        """Value of each entry slot (fp64 stored as two int32 words)."""
+        return self.ent.view(-1, 3)[:, 1:].contiguous().view(torch.float64).view(-1)
 
     def build(self, j0: int) -> None:
         """Build the tile [j0, j0 + tile); tiles must come in ascending order from 0."""
@@ -360,15 +374,14 @@ class TileWeights:
                 "lg_spread_tile_bound")
         torch.cumsum(self.bound, 0, out=self.ptr[1:])
         total = int(self.ptr[-1])  # host sync: sizes the row storage
-        if total > self.col.numel():
-            cap = max(total, int(self.col.numel() * 1.25))
-            self.col = torch.empty(cap, dtype=torch.int32, device=self.dev)
-            self.val = torch.empty(cap, dtype=torch.float64, device=self.dev)
+        if 3 * total > self.ent.numel():
+            cap = max(total, int(self.ent.numel() // 3 * 1.25))
+            self.ent = torch.empty(3 * cap, dtype=torch.int32, device=self.dev)
         N.check(L.lg_spread_tile_weight_f64(
             N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
             N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count), N.ptr(self.alpha),
-            N.ptr(self.beta), j0, self.tile, N.ptr(self.ptr), N.ptr(self.col),
-            N.ptr(self.val), N.ptr(self.len), N.ptr(self.ws), self.ws.numel(), strm),
+            N.ptr(self.beta), j0, self.tile, N.ptr(self.ptr), N.ptr(self.ent),
+            N.ptr(self.meta), N.ptr(self.ws), self.ws.numel(), strm),
             "lg_spread_tile_weight_f64")
         self.j0, self.width = j0, width
 
@@ -376,9 +389,9 @@ class TileWeights:
         """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
         A = self.A
         N.check(N.lib().lg_spread_tile_resource_f64(
-            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), u1 - u0, N.ptr(self.ptr),
-            N.ptr(self.len), N.ptr(self.col), N.ptr(self.val), self.j0, self.tile, N.ptr(out),
-            out.stride(0), N.stream_handle(self.dev)), "lg_spread_tile_resource_f64")
+            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), u1 - u0, N.ptr(self.meta),
+            N.ptr(self.ent), self.j0, self.tile, N.ptr(out), out.stride(0),
+            N.stream_handle(self.dev)), "lg_spread_tile_resource_f64")
         return out
 
 

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--k", type=int, default=20)
     ap.add_argument("--lam", type=float, default=0.5)
     ap.add_argument("--scratch-gib", type=int, default=4)
+    ap.add_argument("--max-tiles", type=int, default=0,
+                    help="stop after this many tiles (quick kernel iteration / profiling); "
+                         "the projection then scales the measured times to all tiles")
     a = ap.parse_args()
     dev = torch.device("cuda")
     U, I, E, D, _ = bench.WORKLOADS[a.workload]
@@ -61,8 +64,9 @@ def main():
     torch.cuda.synchronize()
     wall = time.time()
     last = wall
-    for s0 in range(0, I, span):
-        s1 = min(I, s0 + span)
+    I_run = I if a.max_tiles <= 0 else min(I, a.max_tiles * tile)
+    for s0 in range(0, I_run, span):
+        s1 = min(I_run, s0 + span)
         for j0 in range(s0, s1, tile):
             e0, e1, e2 = ev(), ev(), ev()
             e0.record()
@@ -85,6 +89,8 @@ def main():
             print(f"  tile {tiles} build {t_build:.2f}s resource {t_res:.2f}s topk "
                   f"{t_topk:.2f}s", file=sys.stderr, flush=True)
             last = time.time()
+    scale = -(-I // tile) / tiles
+    t_build, t_res, t_topk = t_build * scale, t_res * scale, t_topk * scale
     t_user = t_res + t_topk
     wall = time.time() - wall
     per_user = t_user / n
