@@ -175,27 +175,26 @@ def bench_small_config(dev, k):
     return res
 
 
-def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, users_per_rank, lam=0.5,
-                 tile=2048):
-    """C5-shape LGCNHS recommendation (SpreadLightGCN, model/SpreadLightGCN/model.py:107-153 +
-    recommend.py:18-52): per user, top-k of G * F with F = A @ HybridS(A, general_W, lam)
-    and G the fp32 e0 score, train|val items dropped; the factored tile path
-    (ops.spread_topk_tiled), users sharded over the ranks with no exchange. Timed end to
-    end: every W tile is built once per rank (user-independent) and applied to the rank's
-    users. Also the Douban-shaped dense path (configs[2]: SpreadLightGCNOpti, lam=0.5)."""
+def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
+    """C5 LGCNHS recommendation for EVERY user (SpreadLightGCN, model/SpreadLightGCN/model.py:
+    107-153 + recommend.py:18-52): per user, top-k of G * F with F = A @ HybridS(A, general_W,
+    lam) and G the fp32 e0 score, train|val items dropped, over the factored tile path.
+    Sharded by item range (lgcnhs.dist.sharded_spread_topk): each rank builds only its own W
+    tiles and scores all users on them, then one all-to-all + merge gives each rank the final
+    lists of its user block. Timed end to end (max over ranks). Also the Douban-shaped dense
+    path (configs[2]: SpreadLightGCNOpti, lam=0.5) at N=1."""
     from lgcnhs import ops
+    from lgcnhs.dist import sharded_spread_topk
     from lgcnhs.synth import synth_interactions
     A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
-    n = min(users_per_rank, -(-U // world))
-    u0 = min(rank * n, U - n)
-    eu = e0_orig[:U]
+    eu = e0_orig[:U].contiguous()
     ei = e0_orig[U:U + I].contiguous()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    _, idx = ops.spread_topk_tiled(A, lam, k, A.by_user, True, eu, ei, users=slice(u0, u0 + n),
-                                   tile=tile)
+    (u0, u1), _, idx = sharded_spread_topk(A, lam, k, A.by_user, True, eu, ei, rank=rank,
+                                           world=world, tile=tile, scratch_bytes=32 << 30)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -205,9 +204,11 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, users_per_rank, lam=0
     filled = float((idx >= 0).float().mean().item())
     del A, idx
     torch.cuda.empty_cache()
-    res = {"recs_per_s": n * world / dt, "users_per_rank": n, "seconds": dt, "k": k,
-           "lambda": lam, "tile": tile, "filled_frac": filled,
-           "path": "lg_spread_tile_{cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 (G by f32 MFMA)"}
+    res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
+           "tile": tile, "filled_frac_rank0": filled,
+           "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
+           "path": "lg_spread_tile_{seek,cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 "
+                   "(G by f32 MFMA) + lg_topk_lists_merge_f64"}
     if world == 1:
         # configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), dense
         # general_W / W (fp64 I x I), fused G * F top-k
@@ -257,8 +258,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-topk", action="store_true")
     ap.add_argument("--no-spread", action="store_true")
-    ap.add_argument("--spread-users", type=int, default=131072,
-                    help="users per rank for the LGCNHS spreading phase")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
@@ -370,8 +369,7 @@ def main():
     spread = None
     if not args.no_spread:
         try:
-            spread = bench_spread(keys, U, I, e0_orig, args.k, rank, world, dev,
-                                  args.spread_users)
+            spread = bench_spread(keys, U, I, e0_orig, args.k, rank, world, dev)
         except Exception as ex:  # a side measurement never hides the main result
             log(f"spread bench failed: {ex!r}")
 

@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 5
+#define LG_ABI_VERSION 6
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -265,6 +265,49 @@ int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int32_t item_
                      const int64_t *ex_rowptr, const int32_t *ex_col, int32_t excl_mode,
                      int32_t k, int32_t first, double *io_val, int64_t *io_idx,
                      lg_stream_t stream);
+
+/* cur[v] = first position of user v's item row (ascending) with item >= item_begin: the
+ * cursor state for a tile walk that starts at item_begin (an item-range shard of a
+ * multi-GPU run) instead of 0. */
+int lg_spread_tile_seek(const int64_t *user_rowptr, const int32_t *user_items,
+                        int64_t n_users, int32_t item_begin, int64_t *cur, lg_stream_t stream);
+
+/* Merge n_lists sorted top-K lists per row, in_val/in_idx laid out [n_lists][n_rows][k]
+ * (value desc, index asc; index -1 = empty), into out_val/out_idx [n_rows][k] in the same
+ * order: the per-item-range lists of lg_tile_topk_f64 (disjoint item ranges) give the lists
+ * a single walk over all items would. k in [1, 128]. */
+int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t n_lists,
+                            int64_t n_rows, int32_t k, double *out_val, int64_t *out_idx,
+                            lg_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Recommendation-list metrics (reference metrics/accurate.py and
+ * metrics/diversity.py). recs is a [n_rows][k] int64 list matrix (recommendDictToTensor,
+ * utils/trans.py:82-92); entries < 0 are padding and match nothing.
+ * ------------------------------------------------------------------------------------ */
+
+/* hit[q * k + p] = 1 if recs[eval_rows[q]][p] is in test row q (pos_rowptr/pos_col: one
+ * sorted row per evaluated user, in eval_rows order), else 0: the `item in items` labels of
+ * calPrecisionAndRecall / calNDCG (metrics/accurate.py:24-31, :69-76). */
+int lg_rec_hits(const int64_t *recs, int64_t n_rows, int32_t k, const int64_t *eval_rows,
+                int64_t n_eval, const int64_t *pos_rowptr, const int32_t *pos_col,
+                uint8_t *hit, lg_stream_t stream);
+
+/* *total = sum over ordered pairs of rows u != v of |set(recs[u]) & set(recs[v])|, computed
+ * exactly as sum_i c_i (c_i - 1) over the per-item list counts c_i (written to counts[n_items],
+ * items >= n_items ignored): calHammingDistance (metrics/diversity.py:15-63) is
+ * 1 - total / (k n_rows (n_rows - 1)). */
+int lg_rec_pair_overlap(const int64_t *recs, int64_t n_rows, int32_t k, int64_t n_items,
+                        int32_t *counts, uint64_t *total, lg_stream_t stream);
+
+/* part[r * k + p] = sum over q > p with recs[r][q] != recs[r][p], both items of nonzero
+ * item_degree, of co(a, b) / sqrt(deg_a * deg_b), co = |users(a) & users(b)| over the item
+ * columns item_rowptr/item_users (sorted) of the binary interaction matrix:
+ * calInternalSimilarity (metrics/diversity.py:66-115) is 2 * sum(part) / (n_rows k (k-1)). */
+int lg_rec_intra_similarity_f64(const int64_t *recs, int64_t n_rows, int32_t k,
+                                const int64_t *item_rowptr, const int32_t *item_users,
+                                const int64_t *item_degree, int64_t n_items, double *part,
+                                lg_stream_t stream);
 
 #ifdef __cplusplus
 }

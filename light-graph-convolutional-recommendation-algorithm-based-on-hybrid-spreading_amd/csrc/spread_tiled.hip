@@ -84,6 +84,17 @@ __global__ __launch_bounds__(256) void k_tile_cursor(const int64_t *__restrict__
   count[v] = (uint16_t)(p - p0);  // <= tile <= 8192
 }
 
+// cur[v] = first position of user v's item row with item >= item_begin: the cursor state
+// of a tile walk that starts at item_begin instead of 0 (an item-range shard).
+__global__ __launch_bounds__(256) void k_tile_seek(const int64_t *__restrict__ user_rowptr,
+                                                   const int32_t *__restrict__ user_items,
+                                                   int64_t n_users, int32_t item_begin,
+                                                   int64_t *__restrict__ cur) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_users) return;
+  cur[v] = lower_bound_i32(user_items, user_rowptr[v], user_rowptr[v + 1], item_begin);
+}
+
 // one wave per item row
 __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ item_rowptr,
                                                     const int32_t *__restrict__ item_users,
@@ -644,9 +655,93 @@ static void launch_tile_topk(int M, const double *F, int64_t ldf, int64_t n_rows
   }
 }
 
+// Merge n_lists sorted top-K lists per row ([n_lists][n_rows][k], index -1 = empty) into one
+// ([n_rows][k]): the item-range shards of a multi-GPU spreading run. One wave per row, the
+// candidate list in LDS (CAP = 64*M >= k + 64), compacted by the wave-wide bitonic sort.
+template <int M>
+__global__ __launch_bounds__(256) void k_lists_merge_f64(const double *__restrict__ in_val,
+                                                         const int64_t *__restrict__ in_idx,
+                                                         int n_lists, int64_t n_rows, int k,
+                                                         double *__restrict__ out_val,
+                                                         int64_t *__restrict__ out_idx) {
+  constexpr int CAP = 64 * M;
+  __shared__ double cs[4][CAP];
+  __shared__ int ci[4][CAP];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= n_rows) return;
+  int cnt = 0;
+  double tau = neg_inf<double>();
+  int tau_id = kPadId;
+  for (int s = 0; s < n_lists; ++s) {
+    const int64_t base = ((int64_t)s * n_rows + row) * k;
+    for (int e0 = 0; e0 < k; e0 += 64) {
+      const int e = e0 + lane;
+      double v = neg_inf<double>();
+      int id = -1;
+      if (e < k) {
+        const int64_t x = in_idx[base + e];
+        if (x >= 0) {
+          v = in_val[base + e];
+          id = (int)x;
+        }
+      }
+      const bool cand = id >= 0 && before(v, id, tau, tau_id);
+      const uint64_t bal = __ballot(cand);
+      const int pos = cnt + __popcll(bal & lanemask_lt());
+      if (cand) {
+        cs[wave][pos] = v;
+        ci[wave][pos] = id;
+      }
+      cnt += __popcll(bal);
+      if (cnt > CAP - 64) {
+        wave_sync();
+        cnt = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+      }
+    }
+  }
+  wave_sync();
+  const int nc = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+  for (int e = lane; e < k; e += 64) {
+    out_val[row * k + e] = e < nc ? cs[wave][e] : neg_inf<double>();
+    out_idx[row * k + e] = e < nc ? ci[wave][e] : -1;
+  }
+}
+
 }  // namespace lg
 
 using namespace lg;
+
+extern "C" int lg_spread_tile_seek(const int64_t *user_rowptr, const int32_t *user_items,
+                                   int64_t n_users, int32_t item_begin, int64_t *cur,
+                                   lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && cur && n_users >= 0 && item_begin >= 0,
+             "lg_spread_tile_seek: bad arguments");
+  if (n_users == 0) return LG_OK;
+  k_tile_seek<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
+      user_rowptr, user_items, n_users, item_begin, cur);
+  return launch_status("lg_spread_tile_seek");
+}
+
+extern "C" int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx,
+                                       int32_t n_lists, int64_t n_rows, int32_t k,
+                                       double *out_val, int64_t *out_idx, lg_stream_t stream) {
+  LG_REQUIRE(n_lists >= 1 && n_rows >= 0, "lg_topk_lists_merge_f64: bad sizes");
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_topk_lists_merge_f64: k=%d not in [1,128]", k);
+  LG_REQUIRE(n_rows == 0 || (in_val && in_idx && out_val && out_idx),
+             "lg_topk_lists_merge_f64: NULL argument");
+  if (n_rows == 0) return LG_OK;
+  const dim3 grid((unsigned)((n_rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  if (k <= 64)
+    k_lists_merge_f64<2><<<grid, dim3(256), 0, s>>>(in_val, in_idx, n_lists, n_rows, k, out_val,
+                                                    out_idx);
+  else
+    k_lists_merge_f64<4><<<grid, dim3(256), 0, s>>>(in_val, in_idx, n_lists, n_rows, k, out_val,
+                                                    out_idx);
+  return launch_status("lg_topk_lists_merge_f64");
+}
 
 extern "C" int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
                                      double *alpha, double *beta, lg_stream_t stream) {

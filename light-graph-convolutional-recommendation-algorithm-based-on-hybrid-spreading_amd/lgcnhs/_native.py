@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "liblgcnhs.so")
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -81,6 +81,12 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _i64, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     ),
+    "lg_spread_tile_seek": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "lg_topk_lists_merge_f64": (ctypes.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "lg_rec_hits": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "lg_rec_pair_overlap": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
+    "lg_rec_intra_similarity_f64": (
+        ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _i64, _vp, _vp]),
 }
 
 _lib = None

@@ -154,3 +154,59 @@ class ShardedPropagation:
             for c in range(sh.chunks):
                 _gather_block(self.out, sh, c, self.group, async_op=False)
         return self.out
+
+
+# ------------------------------------------------------------------ spreading (K3s)
+def item_range(n_items: int, tile: int, rank: int, world: int) -> tuple[int, int]:
+    """Rank r's contiguous run of whole item tiles (the last tile may be short)."""
+    n_tiles = -(-n_items // tile) if n_items else 0
+    t0, t1 = rank * n_tiles // world, (rank + 1) * n_tiles // world
+    return min(n_items, t0 * tile), min(n_items, t1 * tile)
+
+
+def user_block(n_users: int, rank: int, world: int) -> tuple[int, int]:
+    return rank * n_users // world, (rank + 1) * n_users // world
+
+
+def exchange_topk(vals: torch.Tensor, idxs: torch.Tensor, rank: int, world: int,
+                  group=None):
+    """[U, k] lists over this rank's item range, all users -> [world, n_own, k] lists of this
+    rank's user block, one per item range (rank order): one all-to-all (RCCL over xGMI)."""
+    U, k = vals.shape
+    sizes = [user_block(U, r, world)[1] - user_block(U, r, world)[0] for r in range(world)]
+    own = sizes[rank]
+    dev = vals.device
+    if dist.get_backend(group) == "gloo":  # rehearsal backend: host tensors only
+        vals, idxs = vals.cpu(), idxs.cpu()
+    ov = torch.empty((world * own, k), dtype=vals.dtype, device=vals.device)
+    oi = torch.empty((world * own, k), dtype=idxs.dtype, device=idxs.device)
+    dist.all_to_all_single(ov, vals.contiguous(), [own] * world, sizes, group=group)
+    dist.all_to_all_single(oi, idxs.contiguous(), [own] * world, sizes, group=group)
+    return ov.view(world, own, k).to(dev), oi.view(world, own, k).to(dev)
+
+
+def sharded_spread_topk(A, lam: float, k: int, excl, drop: bool = True, eu=None, ei=None,
+                        rank: int = 0, world: int = 1, group=None, tile: int = 2048,
+                        scratch_bytes: int = 16 << 30, local_fn=None, merge_fn=None):
+    """The LGCNHS recommendation (model/SpreadLightGCN/model.py:122-153 + recommend.py:18-52)
+    over `world` GPUs, sharded by ITEM range: rank r builds only its own tiles of W
+    (user-independent work is never repeated across ranks) and scores every user on them;
+    an all-to-all hands each rank the per-range lists of its user block, which are merged.
+    Returns ((u0, u1), values [n_own, k] fp64, items [n_own, k] int64), bitwise the rows
+    [u0, u1) of the single-GPU ops.spread_topk_tiled.
+
+    local_fn / merge_fn default to the HIP path (ops.spread_topk_tiled /
+    ops.merge_topk_lists); tests substitute CPU stand-ins to run the exchange on gloo."""
+    from . import ops
+    local_fn = local_fn or ops.spread_topk_tiled
+    merge_fn = merge_fn or ops.merge_topk_lists
+    i0, i1 = item_range(A.n_items, tile, rank, world)
+    v, i = local_fn(A, lam, k, excl, drop, eu, ei, tile=tile, scratch_bytes=scratch_bytes,
+                    items=slice(i0, i1))
+    u0, u1 = user_block(A.n_users, rank, world)
+    if world == 1:
+        return (u0, u1), v, i
+    pv, pi = exchange_topk(v, i, rank, world, group)
+    del v, i
+    mv, mi = merge_fn(pv, pi)
+    return (u0, u1), mv, mi

@@ -338,6 +338,7 @@ class TileWeights:
         self.ent = torch.empty(0, dtype=torch.int32, device=dev)  # 3 int32 per entry
         self.j0 = None
         self.width = 0
+        self._seek_at = None
 
     @property
     def len(self) -> torch.Tensor:
@@ -354,17 +355,35 @@ class TileWeights:
         """Value of each entry slot (fp64 stored as two int32 words)."""
         return self.ent.view(-1, 3)[:, 1:].contiguous().view(torch.float64).view(-1)
 
-    def build(self, j0: int) -> None:
-        """Build the tile [j0, j0 + tile); tiles must come in ascending order from 0."""
+    def seek(self, j0: int) -> None:
+        """Start the tile walk at item j0 instead of 0 (an item-range shard): the next
+        build() must be build(j0)."""
+        A = self.A
+        if not 0 <= j0 <= A.n_items:
+            raise ValueError(f"seek({j0}) outside [0, {A.n_items}]")
+        N.check(N.lib().lg_spread_tile_seek(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
+                                            A.n_users, j0, N.ptr(self.cur),
+                                            N.stream_handle(self.dev)), "lg_spread_tile_seek")
+        self._seek_at = j0
+
+    def build(self, j0: int, stop: int | None = None) -> None:
+        """Build the tile [j0, min(j0 + tile, stop)); tiles come in ascending order from 0
+        (or from the item given to seek())."""
         A, I, L = self.A, self.A.n_items, N.lib()
         strm = N.stream_handle(self.dev)
-        if j0 == 0:
+        if self._seek_at is not None and j0 == self._seek_at:
+            pass  # cursors placed by seek()
+        elif j0 == 0:
             self.cur.copy_(A.by_user.rowptr[:-1])
-        elif self.j0 is None or j0 != self.j0 + self.tile:
+        elif self.j0 is None or j0 != self.j0 + self.width:
             raise ValueError("tiles must be built in ascending order")
         else:
             self.cur, self.end = self.end, self.cur
-        width = min(self.tile, I - j0)
+        self._seek_at = None
+        stop = I if stop is None else min(int(stop), I)
+        width = min(self.tile, stop - j0)
+        if width <= 0:
+            raise ValueError(f"empty tile at {j0} (stop {stop})")
         N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
                                         A.n_users, j0 + width, N.ptr(self.cur),
                                         N.ptr(self.end), N.ptr(self.count), strm),
@@ -414,7 +433,8 @@ def tile_topk(F: torch.Tensor, j0: int, n_cols: int, k: int, vals: torch.Tensor,
 def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       drop: bool = True, eu: torch.Tensor | None = None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
-                      tile: int = 2048, scratch_bytes: int = 4 << 30):
+                      tile: int = 2048, scratch_bytes: int = 4 << 30,
+                      items: slice | None = None):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). Bitwise the result of
     spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
@@ -422,28 +442,51 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     Each tile of W (user-independent) is built once and applied to all the users; the F
     columns of consecutive tiles are collected in a [users, span] scratch (span = as many
     whole tiles as ``scratch_bytes`` allows) and merged into the running top-k lists once
-    per span. ``users`` restricts the output to a row range (the multi-GPU shard)."""
+    per span. ``users`` restricts the output to a row range; ``items`` restricts the
+    candidates to an item range (the lists of disjoint item ranges merge, with
+    merge_topk_lists, into the full lists: the multi-GPU item shard)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
+    i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
+                                                   min(A.n_items, items.stop))
     n = u1 - u0
     dev = A.k_item.device
     vals = torch.full((n, k), float("-inf"), dtype=torch.float64, device=dev)
     idxs = torch.full((n, k), -1, dtype=torch.int64, device=dev)
-    if n == 0 or A.n_items == 0:
+    if n == 0 or i1 <= i0:
         return vals, idxs
-    tile = min(int(tile), A.n_items)
+    tile = min(int(tile), i1 - i0)
     span = max(tile, scratch_bytes // (n * 8) // tile * tile)
-    span = min(span, -(-A.n_items // tile) * tile)
+    span = min(span, -(-(i1 - i0) // tile) * tile)
     F = torch.empty((n, span), dtype=torch.float64, device=dev)
     tw = TileWeights(A, lam, tile)
+    if i0:
+        tw.seek(i0)
     ex = excl.slice_rows(u0, u1) if excl is not None else None
     eu_r = None if eu is None else eu[u0:u1]
-    for s0 in range(0, A.n_items, span):
-        s1 = min(A.n_items, s0 + span)
+    for s0 in range(i0, i1, span):
+        s1 = min(i1, s0 + span)
         for j0 in range(s0, s1, tile):
-            tw.build(j0)
+            tw.build(j0, stop=i1)
             tw.resource(u0, u1, F[:, j0 - s0:])
-        tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == 0, ex, drop, eu_r, ei)
+        tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
     return vals, idxs
+
+
+def merge_topk_lists(vals: torch.Tensor, idxs: torch.Tensor):
+    """[L, n, k] sorted lists (index -1 = empty) -> the [n, k] top-k of their union, same
+    order (value desc, index asc)."""
+    N.require_gpu(vals, "vals")
+    if vals.dtype != torch.float64 or idxs.dtype != torch.int64 or vals.shape != idxs.shape \
+            or vals.dim() != 3:
+        raise ValueError("merge_topk_lists: vals fp64 / idxs int64 of one [L, n, k] shape")
+    L, n, k = vals.shape
+    vals, idxs = vals.contiguous(), idxs.contiguous()
+    ov = torch.empty((n, k), dtype=torch.float64, device=vals.device)
+    oi = torch.empty((n, k), dtype=torch.int64, device=vals.device)
+    N.check(N.lib().lg_topk_lists_merge_f64(N.ptr(vals), N.ptr(idxs), L, n, k, N.ptr(ov),
+                                            N.ptr(oi), N.stream_handle(vals.device)),
+            "lg_topk_lists_merge_f64")
+    return ov, oi
 
 
 def dense_spread_fits(n_items: int, device, fraction: float = 0.25) -> bool:

@@ -21,6 +21,8 @@ Algorithm-based-on-Hybrid-Spreading @ 2025-12-05; citations are file:line there)
                                         ML-ProbS unfiltered quirk), recommendSpreadMethod
                                         (lambda / transpose overrides)
 * utils/trans.py:13-29,51-80           interaction matrix and user->items dicts
+* metrics/accurate.py:11-102           precision / recall / F1 / NDCG (its fp32 torch ops)
+* metrics/diversity.py:15-115          Hamming distance, internal similarity (its loops)
 
 Pinning: tests/golden/make_golden.py runs the reference's own importable modules
 (SpreadMethod, utils/trans) unmodified, and its LightGCN modules on top of a PyG 2.6.1
@@ -290,3 +292,89 @@ def rows_topk(F: np.ndarray, k: int, ex_rowptr=None, ex_col=None, drop: bool = T
         ov[r, :order.size] = vals[order]
         oi[r, :order.size] = cols[order]
     return ov, oi
+
+
+# ----------------------------------------------------------------------------------
+# metrics: metrics/accurate.py:11-102, metrics/diversity.py:15-115 (the reference's own
+# loop orders and dtypes, so the rounded results agree exactly on the fixtures)
+# ----------------------------------------------------------------------------------
+def _labels(pos: dict, recs: np.ndarray) -> np.ndarray:
+    """metrics/accurate.py:24-31: membership of each recommended item in the user's list."""
+    return np.array([[int(it) in set(int(x) for x in items) for it in recs[uid]]
+                     for uid, items in pos.items()]).astype("float")
+
+
+def precision_recall(pos: dict, recs: np.ndarray, k: int):
+    """metrics/accurate.py:11-46 (fp32 torch reductions, rounded to 5 decimals)."""
+    R = torch.Tensor(_labels(pos, recs))
+    lens = torch.Tensor([len(v) for v in pos.values()])
+    n = torch.sum(R, dim=-1)
+    return round((torch.mean(n) / k).item(), 5), round(torch.mean(n / lens).item(), 5)
+
+
+def f1_score(p: float, r: float) -> float:
+    """metrics/accurate.py:48-56."""
+    return round(2 * (p * r) / (p + r), 5)
+
+
+def ndcg(pos: dict, recs: np.ndarray, k: int) -> float:
+    """metrics/accurate.py:58-102: the ideal DCG counts min(len(list), k) ones, whatever
+    the number of test items."""
+    R = torch.Tensor(_labels(pos, recs))
+    tmp = torch.zeros((len(R), k))
+    for j, row in enumerate(R):
+        tmp[j, :min(len(row), k)] = 1
+    idcg = torch.sum(tmp * 1. / torch.log2(torch.arange(2, k + 2)), axis=1)
+    dcg = torch.sum(R * (1. / torch.log2(torch.arange(2, k + 2))), axis=1)
+    idcg[idcg == 0.] = 1.
+    v = dcg / idcg
+    v[torch.isnan(v)] = 0.
+    return round(torch.mean(v).item(), 5)
+
+
+def hamming_distance(recs: np.ndarray, k: int) -> float:
+    """metrics/diversity.py:15-63: mean over ordered pairs u != v of 1 - |set & set| / k,
+    summed in the reference's (u, v) order."""
+    U = recs.shape[0]
+    sets = [set(int(x) for x in r) for r in recs]
+    total = 0.0
+    for a in range(U):
+        for b in range(U):
+            if a != b:
+                total += 1 - (len(sets[a] & sets[b]) / k)
+    return round(round(total / (U * (U - 1)), 5), 5)
+
+
+def internal_similarity(recs: np.ndarray, deg: dict, A: np.ndarray, k: int) -> float:
+    """metrics/diversity.py:66-115: sum over users and ordered pairs of distinct items of
+    nonzero degree of (A[:, i] . A[:, j]) / sqrt(k_i k_j), in the reference's order."""
+    total = 0.0
+    for row in recs:
+        items = [int(x) for x in row]
+        for i in items:
+            for j in items:
+                if i == j:
+                    continue
+                ki, kj = deg.get(i, 0), deg.get(j, 0)
+                if ki == 0 or kj == 0:
+                    continue
+                total += np.dot(A[:, i], A[:, j]) / np.sqrt(ki * kj)
+    return round(total / (recs.shape[0] * k * (k - 1)), 5)
+
+
+def item_degrees(*pos_dicts: dict) -> dict:
+    """utils/trans.py:94-115 getItemDegreeByUserPosItemDict."""
+    d = {}
+    for pd_ in pos_dicts:
+        for items in pd_.values():
+            for it in items:
+                d[int(it)] = d.get(int(it), 0) + 1
+    return d
+
+
+def pos_dict(pairs: np.ndarray) -> dict:
+    """utils/trans.py:51-63 getUserItemsDictByDataframe on a [2, n] (user, item) array."""
+    d = {}
+    for u, i in zip(pairs[0].tolist(), pairs[1].tolist()):
+        d.setdefault(int(u), []).append(int(i))
+    return d

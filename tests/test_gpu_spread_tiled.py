@@ -149,3 +149,73 @@ def test_spread_method_tiled_dispatch_equals_dense(method, dataset):
                               tiled=t) for t in (False, True)]
     assert torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][0].view(torch.int64), out[1][0].view(torch.int64))
+
+
+def _np_merge(vals, idxs, k):
+    L, n, _ = vals.shape
+    ov = np.full((n, k), -np.inf)
+    oi = np.full((n, k), -1, np.int64)
+    for r in range(n):
+        v, i = vals[:, r].reshape(-1), idxs[:, r].reshape(-1)
+        v, i = v[i >= 0], i[i >= 0]
+        o = np.lexsort((i, -v))[:k]
+        ov[r, :o.size], oi[r, :o.size] = v[o], i[o]
+    return ov, oi
+
+
+@pytest.mark.parametrize("k", [1, 7, 64, 100, 128])
+@pytest.mark.parametrize("L", [1, 3, 8])
+def test_topk_lists_merge_vs_oracle(k, L):
+    """lg_topk_lists_merge_f64 = lexsort (value desc, item asc) of the union, including
+    ties across lists, partially empty and fully empty lists."""
+    from lgcnhs import ops
+    rng = np.random.default_rng(k * 31 + L)
+    n = 300
+    vals = np.full((L, n, k), -np.inf)
+    idxs = np.full((L, n, k), -1, np.int64)
+    for l in range(L):
+        for r in range(n):
+            m = int(rng.integers(0, k + 1)) if r % 5 else (0 if r % 2 else k)
+            ids = rng.choice(np.arange(l * 1000, (l + 1) * 1000), size=m, replace=False)
+            v = rng.integers(0, 6, size=m).astype(np.float64) * 0.25  # many ties
+            o = np.lexsort((ids, -v))
+            vals[l, r, :m], idxs[l, r, :m] = v[o], ids[o]
+    ov, oi = ops.merge_topk_lists(torch.as_tensor(vals).to(DEV), torch.as_tensor(idxs).to(DEV))
+    ev, ei = _np_merge(vals, idxs, k)
+    assert np.array_equal(oi.cpu().numpy(), ei)
+    assert np.array_equal(ov.cpu().numpy(), ev)
+
+
+def test_tile_seek_matches_searchsorted():
+    from lgcnhs import ops
+    A = _inter(400, 900, 9000, seed=4, zipf=True)
+    rp, col = A.by_user.rowptr.cpu().numpy(), A.by_user.col.cpu().numpy()
+    for j0 in (0, 1, 333, 899, 900):
+        tw = ops.TileWeights(A, 0.5, 128)
+        tw.seek(j0)
+        want = [rp[v] + np.searchsorted(col[rp[v]:rp[v + 1]], j0) for v in range(400)]
+        assert np.array_equal(tw.cur.cpu().numpy(), np.array(want))
+
+
+@pytest.mark.parametrize("mode", ["G_drop", "none"])
+@pytest.mark.parametrize("world,tile", [(2, 128), (3, 100), (8, 64), (5, 1000)])
+def test_item_range_shards_merge_to_full(mode, world, tile):
+    """The item-range shards of dist.sharded_spread_topk (each rank's tiles only, all
+    users), merged, equal the single walk over all items bit for bit."""
+    from lgcnhs import ops
+    from lgcnhs.dist import item_range
+    U, I, d, k = 260, 900, 64, 20
+    A = _inter(U, I, 12000, seed=8, zipf=True)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
+    ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
+    kw = dict(eu=eu, ei=ei) if mode == "G_drop" else {}
+    drop = mode != "none"
+    v0, i0 = ops.spread_topk_tiled(A, 0.3, k, A.by_user, drop=drop, tile=tile, **kw)
+    parts = [ops.spread_topk_tiled(A, 0.3, k, A.by_user, drop=drop, tile=tile,
+                                   items=slice(*item_range(I, tile, r, world)), **kw)
+             for r in range(world)]
+    mv, mi = ops.merge_topk_lists(torch.stack([p[0] for p in parts]),
+                                  torch.stack([p[1] for p in parts]))
+    assert torch.equal(mi, i0)
+    assert torch.equal(mv.view(torch.int64), v0.view(torch.int64))
