@@ -110,9 +110,10 @@ def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
 def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
     """Time `steps` full L-layer forwards; returns (max-over-ranks seconds, average SpMM
     'launch' seconds = one layer's kernels on this rank, from HIP events on the stream)."""
-    from lgcnhs.dist import ShardedPropagation
+    from lgcnhs.dist import BipartitePropagation, SegmentShard, ShardedPropagation
     e0 = shard.permute_rows(e0_orig)  # chunk-major layout (identity at N=1)
-    prop = ShardedPropagation(shard, dis_l, D, L, dev)
+    cls = BipartitePropagation if isinstance(shard, SegmentShard) else ShardedPropagation
+    prop = cls(shard, dis_l, D, L, dev)
     for _ in range(warmup):
         prop.forward(e0)
     torch.cuda.synchronize()
@@ -127,13 +128,13 @@ def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t1
-    kernel_ms = [s.elapsed_time(e) for s, e in prop.events]
+    kernel_ms = sum(s.elapsed_time(e) for s, e in prop.events)  # SpMM kernels only
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     del prop, e0
-    return elapsed, sum(kernel_ms) / len(kernel_ms) / 1e3
+    return elapsed, kernel_ms / (steps * L) / 1e3
 
 
 def bench_small_config(dev, k):
@@ -266,7 +267,11 @@ def main():
     ap.add_argument("--extra-dims", type=int, nargs="*", default=[128],
                     help="also time the same graph at these embedding widths")
     ap.add_argument("--chunks", type=int, default=0,
-                    help="sub-chunks per rank per layer for comm/compute overlap (0 = auto)")
+                    help="sub-chunks per rank per layer (per half with --layout bipartite) "
+                         "for comm/compute overlap (0 = auto)")
+    ap.add_argument("--layout", default="bipartite", choices=["bipartite", "rows"],
+                    help="N>1 row sharding: users and items sharded separately with "
+                         "cross-layer overlap (bipartite) or contiguous node rows (rows)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -284,7 +289,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from lgcnhs import ops
-    from lgcnhs.dist import RowShard
+    from lgcnhs.dist import RowShard, SegmentShard
     from lgcnhs.graph import RowSets
 
     U, I, E, D, L = WORKLOADS[args.workload]
@@ -299,8 +304,15 @@ def main():
     wgt = torch.empty(nnz, dtype=torch.float32, device=dev)
     NV.check(NV.lib().lg_gcn_edge_weight_f32(NV.ptr(rowptr), NV.ptr(src), NV.ptr(dis), N, 0,
                                              NV.ptr(wgt), NV.stream_handle(dev)), "edge weights")
-    chunks = args.chunks if args.chunks else (1 if world == 1 else 4)
-    shard = RowShard(rowptr, src, N, rank, world, dev, weight=wgt, chunks=chunks)
+    if world > 1 and args.layout == "bipartite":
+        # users and items sharded separately: one half's all-gather hides behind the other
+        # half's SpMM, across layer boundaries (lgcnhs.dist.BipartitePropagation)
+        chunks = args.chunks if args.chunks else 2
+        shard = SegmentShard(rowptr, src, [0, U, N], rank, world, dev, weight=wgt,
+                             chunks=chunks)
+    else:
+        chunks = args.chunks if args.chunks else (1 if world == 1 else 4)
+        shard = RowShard(rowptr, src, N, rank, world, dev, weight=wgt, chunks=chunks)
     del wgt
     dis_l = shard.permute_rows(dis)
     gen = torch.Generator(device=dev).manual_seed(42)
@@ -310,7 +322,7 @@ def main():
     if cpu_src is None:
         del src
     torch.cuda.synchronize()
-    log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {shard.g0}-{shard.g1} "
+    log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {getattr(shard, 'ranges', None) or (shard.g0, shard.g1)} "
         f"setup {time.time() - t0:.1f}s")
 
     elapsed, avg_kernel_s = time_propagation(shard, dis_l, e0_orig, D, L, args.steps,
@@ -396,7 +408,8 @@ def main():
             "config": {"workload": args.workload, "users": U, "items": I, "interactions": E,
                        "directed_nnz": nnz, "dim": D, "layers": L,
                        "parallelism": f"row-shard x{world} + RCCL all-gather per layer"
-                                      + (f" ({chunks} overlapped sub-chunks)" if world > 1 else "")},
+                                      + (f" ({args.layout} layout, {chunks} sub-chunks)"
+                                         if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel": "lg_spmm_layer_f32",

@@ -280,6 +280,31 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
                             int64_t n_rows, int32_t k, double *out_val, int64_t *out_idx,
                             lg_stream_t stream);
 
+/* Fused lg_spread_tile_resource_f64 + lg_tile_topk_f64 for one tile: each user's F columns
+ * [item_begin, item_begin + width) are accumulated in LDS (same values, bit for bit) and
+ * merged straight into the running top-K lists io_val/io_idx [n_users][k] (first != 0:
+ * start empty); F is never written to memory. G factor: eu = the rows' user embeddings,
+ * ei = all item embeddings, item_norm = lg_row_norms_f64(ei) (|G| <= ||u|| ||i|| bounds the
+ * chain, so columns that cannot beat the K-th value skip the score). Exclusions (dropped):
+ * ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row cursor ex_cur[n_users] positioned
+ * at the walk's first item by lg_spread_tile_seek(ex_rowptr, ex_col, ...) and advanced here.
+ * Walked over tiles in ascending order, the lists equal lg_rows_topk_f64 over the full rows.
+ * k in [1, 128]; dim in {32, 64, 128}; LDS per 2-wave block:
+ * lg_spread_tile_resource_topk_lds_bytes(tile, k, dim or 0). */
+size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
+int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *user_items,
+                                     int64_t n_users, const uint64_t *wt_meta,
+                                     const void *wt_ent, int32_t item_begin, int32_t tile,
+                                     int32_t width, const float *eu, const float *ei,
+                                     int32_t dim, const double *item_norm,
+                                     const int64_t *ex_rowptr, const int32_t *ex_col,
+                                     int64_t *ex_cur, int32_t k, int32_t first,
+                                     double *io_val, int64_t *io_idx, lg_stream_t stream);
+
+/* out[r] = ||x[r]||_2 (fp64) for an fp32 [n_rows, dim] matrix. */
+int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,
+                     lg_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Recommendation-list metrics (reference metrics/accurate.py and
  * metrics/diversity.py). recs is a [n_rows][k] int64 list matrix (recommendDictToTensor,

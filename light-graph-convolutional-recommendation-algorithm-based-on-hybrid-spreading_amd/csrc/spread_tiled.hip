@@ -61,6 +61,19 @@ __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict
   beta[i] = pow(k_item[i], lambda);
 }
 
+// out[r] = ||x[r]||_2 in fp64 (the bound of the fused top-K prefilter).
+__global__ __launch_bounds__(256) void k_row_norms(const float *__restrict__ x, int64_t n,
+                                                   int dim, double *__restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  double s = 0.0;
+  for (int d = 0; d < dim; ++d) {
+    const double v = x[r * dim + d];
+    s += v * v;
+  }
+  out[r] = sqrt(s);
+}
+
 __global__ __launch_bounds__(256) void k_inv_degree(const int64_t *__restrict__ rowptr,
                                                     int64_t n, double *__restrict__ inv) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -308,22 +321,19 @@ __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ wt
 constexpr int kResRows = 128;
 constexpr int kResIdxBytes = kResRows * (4 + 8);
 
+// acc[j - item_begin] += W[i][j] for every item i of user u (ascending), acc = the wave's
+// LDS tile accumulator (zeroed by the caller), idx = its kResIdxBytes row index.
 template <int UF>
-__global__ __launch_bounds__(256) void k_tile_resource(
-    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
-    int32_t item_begin, int32_t tile, double *__restrict__ F, int64_t ldf) {
-  extern __shared__ double lds[];
-  const int wave = threadIdx.x / 64;
-  const int wpb = blockDim.x / 64;
+__device__ __forceinline__ void accumulate_user_tile(double *acc, char *idx,
+                                                     const int64_t *__restrict__ user_rowptr,
+                                                     const int32_t *__restrict__ user_items,
+                                                     int64_t u,
+                                                     const uint64_t *__restrict__ wt_meta,
+                                                     const WEnt *__restrict__ wt_ent,
+                                                     int32_t item_begin) {
   const int lane = lane_id();
-  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
-  if (u >= n_users) return;
-  double *acc = lds + (int64_t)wave * tile;
-  char *idx = reinterpret_cast<char *>(lds + (int64_t)wpb * tile) + wave * kResIdxBytes;
   int64_t *s_base = reinterpret_cast<int64_t *>(idx);               // entry e of row r: base_r + e
   int *s_incl = reinterpret_cast<int *>(idx + kResRows * 8);         // inclusive entry prefix
-  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
   const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
   for (int64_t p0 = pb; p0 < pe; p0 += kResRows) {
     uint64_t m0 = 0, m1 = 0;
@@ -377,6 +387,23 @@ __global__ __launch_bounds__(256) void k_tile_resource(
     }
   }
   wave_sync();
+}
+
+template <int UF>
+__global__ __launch_bounds__(256) void k_tile_resource(
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
+    int32_t item_begin, int32_t tile, double *__restrict__ F, int64_t ldf) {
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x / 64;
+  const int wpb = blockDim.x / 64;
+  const int lane = lane_id();
+  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
+  if (u >= n_users) return;
+  double *acc = lds + (int64_t)wave * tile;
+  char *idx = reinterpret_cast<char *>(lds + (int64_t)wpb * tile) + wave * kResIdxBytes;
+  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
+  accumulate_user_tile<UF>(acc, idx, user_rowptr, user_items, u, wt_meta, wt_ent, item_begin);
   double *row = F + u * ldf;
   for (int j = lane; j < tile; j += 64) row[j] = acc[j];
 }
@@ -633,6 +660,153 @@ __global__ __launch_bounds__(128) void k_tile_topk(
   }
 }
 
+// fp32 score of one (user, item) pair: the chain of lg_score_topk_f32 / the MFMA tile,
+//   acc = 0; for s < D/4: for g < 4: acc = fmaf(u[g*D/4+s], i[g*D/4+s], acc),
+// with u in LDS (read as a broadcast) and the item row from global memory.
+template <int D>
+__device__ __forceinline__ float chain_score(const float *us, const float *__restrict__ it) {
+  constexpr int Q = D / 4;
+  float a = 0.f;
+#pragma unroll
+  for (int s0 = 0; s0 < Q; s0 += 4) {
+    float4 q[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) q[g] = *reinterpret_cast<const float4 *>(it + g * Q + s0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float x = s == 0 ? q[g].x : (s == 1 ? q[g].y : (s == 2 ? q[g].z : q[g].w));
+        a = fmaf(us[g * Q + s0 + s], x, a);
+      }
+  }
+  return a;
+}
+
+// Per-wave LDS of the fused kernel: the tile accumulator, the row index of
+// accumulate_user_tile, the candidate list (CAP values + ids) and the user's embedding.
+__host__ __device__ constexpr size_t fused_wave_bytes(int tile, int M, int D) {
+  return (size_t)tile * 8 + kResIdxBytes + (size_t)64 * M * 12 + (size_t)D * 4;
+}
+
+// Fused resource + top-K for one tile (lg_spread_tile_resource_topk_f64): one wave per user.
+// The user's F columns [item_begin, item_begin + width) are accumulated in LDS exactly as
+// k_tile_resource does, the user's excluded items in the tile are marked (-1: F >= 0
+// otherwise), and the columns merge straight into the running list: a column can only enter
+// if (G *) F beats the current K-th value tau. With a G factor, |G| <= ||u|| ||i|| (1 + 1e-4)
+// bounds the fp32 chain (its rounding is < 64 * 2^-24 relative), so once tau > 0 a column
+// with F * bound <= tau is skipped without computing G; the rest get the exact chain score.
+// Ids grow along the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
+template <int UF, int D, int M>
+__global__ __launch_bounds__(128) void k_tile_resource_topk(
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
+    int32_t item_begin, int32_t tile, int32_t width, const float *__restrict__ eu,
+    const float *__restrict__ ei, const double *__restrict__ item_norm,
+    const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col,
+    int64_t *__restrict__ ex_cur, int k, int first, double *__restrict__ io_val,
+    int64_t *__restrict__ io_idx) {
+  constexpr int CAP = 64 * M;
+  extern __shared__ double lds[];
+  const int wave = threadIdx.x / 64;
+  const int wpb = blockDim.x / 64;
+  const int lane = lane_id();
+  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
+  if (u >= n_users) return;
+  char *mine = reinterpret_cast<char *>(lds) + (size_t)wave * fused_wave_bytes(tile, M, D);
+  double *acc = reinterpret_cast<double *>(mine);
+  char *idx = mine + (size_t)tile * 8;
+  double *cs = reinterpret_cast<double *>(idx + kResIdxBytes);
+  int *ci = reinterpret_cast<int *>(cs + CAP);
+  float *us = reinterpret_cast<float *>(ci + CAP);
+
+  // running list (sorted, valid entries first)
+  int cnt = 0;
+  double tau = neg_inf<double>();
+  int tau_id = kPadId;
+  if (!first) {
+    for (int e0 = 0; e0 < k; e0 += 64) {
+      const int e = e0 + lane;
+      const int64_t id = e < k ? io_idx[u * k + e] : -1;
+      if (id >= 0) {
+        cs[e] = io_val[u * k + e];
+        ci[e] = (int)id;
+      }
+      cnt += __popcll(__ballot(id >= 0));
+    }
+  }
+  double ubound = 0.0;
+  if constexpr (D > 0) {
+    double ss = 0.0;
+    for (int d = lane; d < D; d += 64) {
+      const float x = eu[u * D + d];
+      us[d] = x;
+      ss += (double)x * (double)x;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    ubound = sqrt(ss) * (1.0 + 1e-4);
+  }
+  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
+  // (accumulate_user_tile's first barrier orders the list / embedding / zero stores)
+  accumulate_user_tile<UF>(acc, idx, user_rowptr, user_items, u, wt_meta, wt_ent, item_begin);
+  if (cnt == k) {
+    tau = cs[k - 1];
+    tau_id = ci[k - 1];
+  }
+  const int lim = item_begin + width;
+  if (ex_rowptr) {
+    // excluded items of the tile: the next run of the user's sorted exclusion row
+    int64_t pos = ex_cur[u];
+    const int64_t hi = ex_rowptr[u + 1];
+    while (pos < hi) {
+      const int64_t e = pos + lane;
+      const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+      const bool in = x < lim;
+      if (in && x >= item_begin) acc[x - item_begin] = -1.0;
+      const int nin = __popcll(__ballot(in));
+      pos += nin;
+      if (nin < 64) break;
+    }
+    if (lane == 0) ex_cur[u] = pos;
+    wave_sync();
+  }
+  for (int c0 = 0; c0 < width; c0 += 64) {
+    const int j = c0 + lane;
+    const double f = j < width ? acc[j] : -1.0;
+    bool cand = f >= 0.0;
+    double v = f;
+    if constexpr (D > 0) {
+      if (cand && tau > 0.0) cand = f * (ubound * item_norm[item_begin + j]) > tau;
+      if (__ballot(cand)) {
+        if (cand) v = (double)chain_score<D>(us, ei + (int64_t)(item_begin + j) * D) * f;
+        cand = cand && v > tau;
+      }
+    } else {
+      cand = cand && v > tau;
+    }
+    const uint64_t bal = __ballot(cand);
+    if (bal) {
+      const int p = cnt + __popcll(bal & lanemask_lt());
+      if (cand) {
+        cs[p] = v;
+        ci[p] = item_begin + j;
+      }
+      cnt += __popcll(bal);
+      if (cnt > CAP - 64) {
+        wave_sync();
+        cnt = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
+      }
+    }
+  }
+  wave_sync();
+  const int nc = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
+  for (int e = lane; e < k; e += 64) {
+    io_val[u * k + e] = e < nc ? cs[e] : neg_inf<double>();
+    io_idx[u * k + e] = e < nc ? ci[e] : -1;
+  }
+}
+
 template <int D>
 static void launch_tile_topk(int M, const double *F, int64_t ldf, int64_t n_rows, int32_t j0,
                              int32_t n_cols, const float *eu, const float *ei,
@@ -874,4 +1048,70 @@ extern "C" int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows,
     default: launch_tile_topk<128>(M, F, ldf, n_rows, item_begin, n_cols, eu, ei, ex_rowptr, ex_col, drop, k, first, io_val, io_idx, s); break;
   }
   return launch_status("lg_tile_topk_f64");
+}
+
+extern "C" size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim) {
+  const int M = k <= 64 ? 2 : 4;
+  return 2 * fused_wave_bytes(tile, M, dim);
+}
+
+template <int D>
+static void launch_fused(int M, const int64_t *user_rowptr, const int32_t *user_items,
+                         int64_t n_users, const uint64_t *wt_meta, const WEnt *wt_ent,
+                         int32_t item_begin, int32_t tile, int32_t width, const float *eu,
+                         const float *ei, const double *item_norm, const int64_t *ex_rowptr,
+                         const int32_t *ex_col, int64_t *ex_cur, int k, int first,
+                         double *io_val, int64_t *io_idx, hipStream_t s) {
+  const unsigned b = (unsigned)((n_users + 1) / 2);
+  const size_t lds = 2 * fused_wave_bytes(tile, M, D);
+  if (M == 2)
+    k_tile_resource_topk<16, D, 2><<<b, 128, lds, s>>>(
+        user_rowptr, user_items, n_users, wt_meta, wt_ent, item_begin, tile, width, eu, ei,
+        item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx);
+  else
+    k_tile_resource_topk<16, D, 4><<<b, 128, lds, s>>>(
+        user_rowptr, user_items, n_users, wt_meta, wt_ent, item_begin, tile, width, eu, ei,
+        item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx);
+}
+
+extern "C" int lg_spread_tile_resource_topk_f64(
+    const int64_t *user_rowptr, const int32_t *user_items, int64_t n_users,
+    const uint64_t *wt_meta, const void *wt_ent, int32_t item_begin, int32_t tile,
+    int32_t width, const float *eu, const float *ei, int32_t dim, const double *item_norm,
+    const int64_t *ex_rowptr, const int32_t *ex_col, int64_t *ex_cur, int32_t k,
+    int32_t first, double *io_val, int64_t *io_idx, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && wt_meta && io_val && io_idx && n_users >= 0 && item_begin >= 0,
+             "lg_spread_tile_resource_topk_f64: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile &&
+                 (int64_t)item_begin + width < 0x7fffffff,
+             "lg_spread_tile_resource_topk_f64: tile %d / width %d", tile, width);
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_spread_tile_resource_topk_f64: k=%d not in [1,128]", k);
+  LG_REQUIRE(!eu == !ei && (!eu || item_norm),
+             "lg_spread_tile_resource_topk_f64: eu, ei and item_norm go together");
+  LG_REQUIRE(!eu || dim == 32 || dim == 64 || dim == 128,
+             "lg_spread_tile_resource_topk_f64: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(!ex_rowptr == !ex_col && !ex_rowptr == !ex_cur,
+             "lg_spread_tile_resource_topk_f64: ex_rowptr/ex_col/ex_cur go together");
+  LG_REQUIRE(lg_spread_tile_resource_topk_lds_bytes(tile, k, eu ? dim : 0) <= 160 * 1024,
+             "lg_spread_tile_resource_topk_f64: tile %d needs too much LDS", tile);
+  if (n_users == 0) return LG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int M = k <= 64 ? 2 : 4;
+  const WEnt *w = (const WEnt *)wt_ent;
+  switch (eu ? dim : 0) {
+    case 0: launch_fused<0>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
+    case 32: launch_fused<32>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
+    case 64: launch_fused<64>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
+    default: launch_fused<128>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
+  }
+  return launch_status("lg_spread_tile_resource_topk_f64");
+}
+
+extern "C" int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,
+                                lg_stream_t stream) {
+  LG_REQUIRE(x && out && n_rows >= 0 && dim >= 1, "lg_row_norms_f64: bad arguments");
+  if (n_rows == 0) return LG_OK;
+  k_row_norms<<<dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
+      x, n_rows, dim, out);
+  return launch_status("lg_row_norms_f64");
 }

@@ -83,6 +83,12 @@ SIGNATURES = {
     ),
     "lg_spread_tile_seek": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "lg_topk_lists_merge_f64": (ctypes.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "lg_spread_tile_resource_topk_lds_bytes": (_sz, [_i32, _i32, _i32]),
+    "lg_spread_tile_resource_topk_f64": (
+        ctypes.c_int,
+        [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32,
+         _i32, _vp, _vp, _vp]),
+    "lg_row_norms_f64": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "lg_rec_hits": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     "lg_rec_pair_overlap": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
     "lg_rec_intra_similarity_f64": (

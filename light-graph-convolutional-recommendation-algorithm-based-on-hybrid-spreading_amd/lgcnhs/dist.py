@@ -156,6 +156,180 @@ class ShardedPropagation:
         return self.out
 
 
+# ------------------------------------------------------- bipartite-ordered propagation
+class SegmentShard:
+    """This rank's rows when the node ids form contiguous segments that are sharded
+    separately: for LightGCN, users [0, U) and items [U, U+I). Rank r owns sub-chunk r of
+    every segment (a share of the users AND a share of the items), each cut into C pieces of
+    S_s rows. Layout: segment-major, then chunk-major inside a segment,
+        new(g) = base_s + c*(W*S_s) + r*S_s + i     for g = start_s + r*(C*S_s) + c*S_s + i,
+    so piece (s, c) of every rank is one contiguous block that all_gather_into_tensor writes
+    in place. Exposes the interface of RowShard (rowptr/src/weight/pieces, to_layout,
+    permute_rows) plus ``seg_pieces[s]``."""
+
+    def __init__(self, rowptr: torch.Tensor, src: torch.Tensor, bounds: list, rank: int,
+                 world: int, device=None, weight: torch.Tensor | None = None,
+                 chunks: int = 1):
+        self.bounds = [int(b) for b in bounds]
+        self.n_nodes = self.bounds[-1]
+        self.rank, self.world, self.chunks = rank, world, chunks
+        dev = device if device is not None else rowptr.device
+        self.device = dev
+        W, C = world, chunks
+        nseg = len(self.bounds) - 1
+        self.S, self.base = [], []
+        base = 0
+        for s in range(nseg):
+            n_s = self.bounds[s + 1] - self.bounds[s]
+            S_s = math.ceil(n_s / (W * C)) if n_s else 0
+            self.S.append(S_s)
+            self.base.append(base)
+            base += W * C * S_s
+        self.n_pad = base
+        rp_parts, src_parts, w_parts = [], [], []
+        self.seg_pieces, self.ranges = [], []
+        lrow, lent = 0, 0
+        for s in range(nseg):
+            st, en, S_s = self.bounds[s], self.bounds[s + 1], self.S[s]
+            g0 = min(st + rank * C * S_s, en)
+            g1 = min(en, g0 + C * S_s)
+            self.ranges.append((g0, g1))
+            b, e = int(rowptr[g0]), int(rowptr[g1])
+            rp_parts.append((rowptr[g0:g1] - b + lent) if g1 > g0 else rowptr[:0])
+            src_parts.append(src[b:e])
+            if weight is not None:
+                w_parts.append(weight[b:e])
+            pieces = []
+            for c in range(C):
+                lb = min(c * S_s, g1 - g0)
+                le = min((c + 1) * S_s, g1 - g0)
+                pieces.append((lrow + lb, lrow + le, self.base[s] + c * W * S_s + rank * S_s))
+            self.seg_pieces.append(pieces)
+            lrow += g1 - g0
+            lent += e - b
+        self.rowptr = torch.cat(rp_parts + [torch.tensor([lent], dtype=rowptr.dtype,
+                                                         device=rowptr.device)]).to(dev)
+        self.nnz = lent
+        src_local = torch.cat(src_parts).to(dev)
+        self.src = self.to_layout(src_local.to(torch.int64)).to(torch.int32)
+        self.weight = None if weight is None else torch.cat(w_parts).to(dev)
+        self.pieces = [p for ps in self.seg_pieces for p in ps]
+        self._n_rows = lrow
+
+    @property
+    def n_rows(self) -> int:
+        return self._n_rows
+
+    def to_layout(self, g: torch.Tensor) -> torch.Tensor:
+        """original node id -> layout id."""
+        b = torch.tensor(self.bounds[1:-1], dtype=torch.int64, device=g.device)
+        seg = torch.bucketize(g, b, right=True)
+        st = torch.tensor(self.bounds[:-1], dtype=torch.int64, device=g.device)[seg]
+        S = torch.tensor(self.S, dtype=torch.int64, device=g.device)[seg].clamp_min(1)
+        base = torch.tensor(self.base, dtype=torch.int64, device=g.device)[seg]
+        o = g - st
+        CS = self.chunks * S
+        r, rem = o // CS, o % CS
+        c, i = rem // S, rem % S
+        return base + c * (self.world * S) + r * S + i
+
+    def permute_rows(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.zeros((self.n_pad,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        out[self.to_layout(torch.arange(self.n_nodes, device=t.device))] = t
+        return out
+
+    def unpermute_rows(self, t: torch.Tensor) -> torch.Tensor:
+        return t[self.to_layout(torch.arange(self.n_nodes, device=t.device))]
+
+    def is_bipartite(self) -> bool:
+        """True when the rows of each of two segments only reference the other segment."""
+        if len(self.bounds) != 3:
+            return False
+        split = self.base[1]  # layout ids below this belong to segment 0
+        for s, pieces in enumerate(self.seg_pieces):
+            lb, le = pieces[0][0], pieces[-1][1]
+            if le <= lb:
+                continue
+            ids = self.src[int(self.rowptr[lb]):int(self.rowptr[le])]
+            if ids.numel() and bool(((ids < split) if s == 0 else (ids >= split)).any()):
+                return False
+        return True
+
+
+def _gather_piece(buf: torch.Tensor, shard: SegmentShard, s: int, c: int, group=None,
+                  async_op=True):
+    W, S, base = shard.world, shard.S[s], shard.base[s]
+    blk = buf[base + c * W * S:base + (c + 1) * W * S]
+    mine = blk[shard.rank * S:(shard.rank + 1) * S]
+    if dist.get_backend(group) == "gloo":
+        return dist.all_gather([blk[r * S:(r + 1) * S] for r in range(W)], mine.clone(),
+                               group=group, async_op=async_op)
+    return dist.all_gather_into_tensor(blk, mine, group=group, async_op=async_op)
+
+
+class BipartitePropagation:
+    """mean_{l<=L} A_hat^l e0 over a SegmentShard of the user-item graph, with the
+    all-gathers overlapped ACROSS layer boundaries. User rows read only item rows and vice
+    versa, so a layer computes one half, starts its gathers, and computes the other half;
+    the next layer starts with the half whose input was gathered first:
+        layer 0: items, users      layer 1: users, items      layer 2: items, users ...
+    Before computing a half only the gathers of its input half are awaited, so the
+    exchange of one half hides behind the computation of the other and the chain of
+    gathers never waits for a whole layer. (Graphs that are not bipartite over the two
+    segments wait for every pending gather.)"""
+
+    def __init__(self, shard: SegmentShard, dis_layout: torch.Tensor, dim: int, layers: int,
+                 device, layer_fn=hip_layer, group=None):
+        self.shard, self.dis, self.layers, self.group = shard, dis_layout, layers, group
+        self.layer_fn = layer_fn
+        n_pad = shard.n_pad
+        self.bufs = [torch.zeros(n_pad, dim, device=device),
+                     torch.zeros(n_pad, dim, device=device) if layers > 2 else None]
+        self.out = torch.zeros(n_pad, dim, device=device)
+        self.bipartite = shard.is_bipartite()
+        self.events = None  # optional list of (start, end) event pairs: one per layer half
+
+    def forward(self, e0_layout: torch.Tensor, gather_out: bool = False) -> torch.Tensor:
+        sh = self.shard
+        x = e0_layout
+        L = self.layers
+        nseg = len(sh.seg_pieces)
+        pending = {}
+        for l in range(L):
+            last = l == L - 1
+            y = None if last else self.bufs[l % 2]
+            mode = acc_mode(l, L)
+            order = [1, 0] if (l % 2 == 0 and nseg == 2) else list(range(nseg))
+            fresh = {}
+            for s in order:
+                need = [1 - s] if (self.bipartite and nseg == 2) else list(pending)
+                for q in need:
+                    for h in pending.pop(q, []):
+                        h.wait()
+                if self.events is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                for c, piece in enumerate(sh.seg_pieces[s]):
+                    self.layer_fn(sh, piece, self.dis, x, y, e0_layout, self.out, self.out,
+                                  mode, L + 1)
+                    if not last and sh.world > 1:
+                        fresh.setdefault(s, []).append(_gather_piece(y, sh, s, c, self.group))
+                if self.events is not None:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record()
+                    self.events.append((ev0, ev1))
+            for hs in pending.values():  # (non-bipartite leftovers)
+                for h in hs:
+                    h.wait()
+            pending = fresh
+            x = y
+        if gather_out and sh.world > 1:
+            for s, pieces in enumerate(sh.seg_pieces):
+                for c in range(len(pieces)):
+                    _gather_piece(self.out, sh, s, c, self.group, async_op=False)
+        return self.out
+
+
 # ------------------------------------------------------------------ spreading (K3s)
 def item_range(n_items: int, tile: int, rank: int, world: int) -> tuple[int, int]:
     """Rank r's contiguous run of whole item tiles (the last tile may be short)."""

@@ -434,7 +434,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       drop: bool = True, eu: torch.Tensor | None = None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
                       tile: int = 2048, scratch_bytes: int = 4 << 30,
-                      items: slice | None = None):
+                      items: slice | None = None, fused: bool | None = None):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). Bitwise the result of
     spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
@@ -444,7 +444,13 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     whole tiles as ``scratch_bytes`` allows) and merged into the running top-k lists once
     per span. ``users`` restricts the output to a row range; ``items`` restricts the
     candidates to an item range (the lists of disjoint item ranges merge, with
-    merge_topk_lists, into the full lists: the multi-GPU item shard)."""
+    merge_topk_lists, into the full lists: the multi-GPU item shard). fused=True merges each
+    tile's columns into the lists inside the resource kernel
+    (lg_spread_tile_resource_topk_f64): F never leaves LDS and no scratch is used. It is the
+    default without a G factor; with one (SpreadLightGCN), the score of every surviving
+    column must be computed per user from global item rows, which costs more than the F
+    round trip (C5: 14.4 s fused vs 8.1 s with the 16-user MFMA tiles of lg_tile_topk_f64),
+    so the default there is the two-kernel path."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -455,14 +461,19 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     if n == 0 or i1 <= i0:
         return vals, idxs
     tile = min(int(tile), i1 - i0)
-    span = max(tile, scratch_bytes // (n * 8) // tile * tile)
-    span = min(span, -(-(i1 - i0) // tile) * tile)
-    F = torch.empty((n, span), dtype=torch.float64, device=dev)
     tw = TileWeights(A, lam, tile)
     if i0:
         tw.seek(i0)
     ex = excl.slice_rows(u0, u1) if excl is not None else None
     eu_r = None if eu is None else eu[u0:u1]
+    if fused is None:
+        fused = eu is None
+    if fused:
+        _fused_walk(A, tw, u0, u1, i0, i1, k, ex if drop else None, eu_r, ei, vals, idxs)
+        return vals, idxs
+    span = max(tile, scratch_bytes // (n * 8) // tile * tile)
+    span = min(span, -(-(i1 - i0) // tile) * tile)
+    F = torch.empty((n, span), dtype=torch.float64, device=dev)
     for s0 in range(i0, i1, span):
         s1 = min(i1, s0 + span)
         for j0 in range(s0, s1, tile):
@@ -470,6 +481,43 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
             tw.resource(u0, u1, F[:, j0 - s0:])
         tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
     return vals, idxs
+
+
+def row_norms(x: torch.Tensor) -> torch.Tensor:
+    """fp64 L2 norm of each row of an fp32 matrix."""
+    x = _f32(x, "x")
+    out = torch.empty(x.shape[0], dtype=torch.float64, device=x.device)
+    N.check(N.lib().lg_row_norms_f64(N.ptr(x), x.shape[0], x.shape[1], N.ptr(out),
+                                     N.stream_handle(x.device)), "lg_row_norms_f64")
+    return out
+
+
+def _fused_walk(A: Interactions, tw: TileWeights, u0: int, u1: int, i0: int, i1: int, k: int,
+                ex: RowSets | None, eu, ei, vals: torch.Tensor, idxs: torch.Tensor) -> None:
+    """Tiles [i0, i1) of the factored spreading with the top-K merge fused into the resource
+    pass (one lg_spread_tile_resource_topk_f64 per tile)."""
+    n = u1 - u0
+    dev = vals.device
+    strm = N.stream_handle(dev)
+    d, norms = 0, None
+    if eu is not None:
+        eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
+        d = eu.shape[1]
+        norms = row_norms(ei)
+    ex_cur = None
+    if ex is not None:
+        ex_cur = torch.empty(n, dtype=torch.int64, device=dev)
+        N.check(N.lib().lg_spread_tile_seek(N.ptr(ex.rowptr), N.ptr(ex.col), n, i0,
+                                            N.ptr(ex_cur), strm), "lg_spread_tile_seek")
+    rp = A.by_user.rowptr[u0:]
+    for j0 in range(i0, i1, tw.tile):
+        tw.build(j0, stop=i1)
+        N.check(N.lib().lg_spread_tile_resource_topk_f64(
+            N.ptr(rp), N.ptr(A.by_user.col), n, N.ptr(tw.meta), N.ptr(tw.ent), j0, tw.tile,
+            tw.width, N.ptr(eu), N.ptr(ei), d, N.ptr(norms),
+            N.ptr(ex.rowptr if ex is not None else None), N.ptr(ex.col if ex is not None else None),
+            N.ptr(ex_cur), int(k), int(j0 == i0), N.ptr(vals), N.ptr(idxs), strm),
+            "lg_spread_tile_resource_topk_f64")
 
 
 def merge_topk_lists(vals: torch.Tensor, idxs: torch.Tensor):

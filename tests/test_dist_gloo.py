@@ -45,7 +45,7 @@ def cpu_layer(shard, piece, dis, x, y, x0, acc, out, mode, denom):
             out[g] = (x0[g] + v) / denom
 
 
-def _worker(rank, world, port, U, I, users, items, layers, chunks, q):
+def _worker(rank, world, port, U, I, users, items, layers, chunks, q, bipartite=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,11 +59,19 @@ def _worker(rank, world, port, U, I, users, items, layers, chunks, q):
         deg = (rowptr[1:] - rowptr[:-1]).float()
         dis = deg.pow(-0.5)
         dis.masked_fill_(dis == float("inf"), 0)
-        shard = RowShard(rowptr, src, n, rank, world, "cpu", chunks=chunks)
         torch.manual_seed(0)
-        e0 = shard.permute_rows(torch.randn(n, 8) * 0.1)
-        prop = ShardedPropagation(shard, shard.permute_rows(dis), 8, layers, "cpu",
-                                  layer_fn=cpu_layer)
+        if bipartite:
+            from lgcnhs.dist import BipartitePropagation, SegmentShard
+            shard = SegmentShard(rowptr, src, [0, U, n], rank, world, "cpu", chunks=chunks)
+            assert shard.is_bipartite()
+            e0 = shard.permute_rows(torch.randn(n, 8) * 0.1)
+            prop = BipartitePropagation(shard, shard.permute_rows(dis), 8, layers, "cpu",
+                                        layer_fn=cpu_layer)
+        else:
+            shard = RowShard(rowptr, src, n, rank, world, "cpu", chunks=chunks)
+            e0 = shard.permute_rows(torch.randn(n, 8) * 0.1)
+            prop = ShardedPropagation(shard, shard.permute_rows(dis), 8, layers, "cpu",
+                                      layer_fn=cpu_layer)
         out = prop.forward(e0, gather_out=True)
         if rank == 0:
             q.put(shard.unpermute_rows(out).numpy().copy())
@@ -71,15 +79,19 @@ def _worker(rank, world, port, U, I, users, items, layers, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,layers,chunks", [(2, 3, 1), (2, 1, 1), (3, 2, 1), (2, 3, 3),
-                                                (3, 3, 2), (1, 3, 4)])
-def test_sharded_propagation_gloo(world, layers, chunks):
+@pytest.mark.parametrize("world,layers,chunks,bipartite",
+                         [(2, 3, 1, False), (2, 1, 1, False), (3, 2, 1, False),
+                          (2, 3, 3, False), (3, 3, 2, False), (1, 3, 4, False),
+                          (2, 3, 1, True), (3, 4, 1, True), (2, 2, 3, True), (4, 3, 2, True),
+                          (1, 3, 1, True)])
+def test_sharded_propagation_gloo(world, layers, chunks, bipartite):
     U, I = 13, 17
     users, items = O.coo_to_interactions(U, I, O.coo_adjacency(U, I, *np.random.default_rng(1).integers(0, [U, I], (60, 2)).T))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, U, I, users, items, layers, chunks, q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, U, I, users, items, layers, chunks, q, bipartite))
              for r in range(world)]
     for p in procs:
         p.start()

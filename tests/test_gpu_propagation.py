@@ -200,3 +200,32 @@ def test_captured_graph_replay_matches_eager():
     for seed in (0, 1):
         e0 = torch.randn(943 + 1682, 64, device=DEV, generator=torch.Generator(device=DEV).manual_seed(seed)) * 0.1
         assert torch.equal(pg.run(e0).clone(), ops.propagate(adj, e0, 3))
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+@pytest.mark.parametrize("cls", ["rows", "bipartite"])
+def test_sharded_layouts_single_rank_equal_propagate(cls, chunks):
+    """The multi-GPU drivers (lgcnhs.dist) on the HIP layer at world 1: the chunk-major and
+    the bipartite segment layouts (users / items sharded separately, half order alternating
+    per layer) give exactly ops.propagate's result."""
+    from lgcnhs import ops
+    from lgcnhs.dist import (BipartitePropagation, RowShard, SegmentShard,
+                             ShardedPropagation)
+    from lgcnhs.graph import Adjacency
+    from lgcnhs.synth import synth_interactions
+    U, I, d, L = 3000, 2000, 64, 3
+    u, i = synth_interactions(U, I, 40000, seed=6, dist="zipf")
+    adj = Adjacency.from_interactions(torch.as_tensor(u), torch.as_tensor(i), U, I, "cuda")
+    e0 = torch.randn(U + I, d, device="cuda", generator=torch.Generator("cuda").manual_seed(1)) * 0.1
+    want = ops.propagate(adj, e0, L)
+    w = adj.edge_weight()
+    if cls == "rows":
+        sh = RowShard(adj.rowptr, adj.src, U + I, 0, 1, "cuda", weight=w, chunks=chunks)
+        prop = ShardedPropagation(sh, sh.permute_rows(adj.dis()), d, L, "cuda")
+    else:
+        sh = SegmentShard(adj.rowptr, adj.src, [0, U, U + I], 0, 1, "cuda", weight=w,
+                          chunks=chunks)
+        assert sh.is_bipartite()
+        prop = BipartitePropagation(sh, sh.permute_rows(adj.dis()), d, L, "cuda")
+    got = sh.unpermute_rows(prop.forward(sh.permute_rows(e0)))
+    assert torch.equal(got, want)

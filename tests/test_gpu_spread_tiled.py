@@ -75,11 +75,13 @@ def test_spread_topk_tiled_equals_dense(k, tile, mode):
     kw = dict(eu=eu if use_g else None, ei=ei if use_g else None)
     v0, i0 = ops.spread_topk(A, W, k, A.by_user, drop=drop, **kw)
     # scratch for one tile (span = tile) and for several tiles per top-k merge
-    for scratch in (1, 3 * U * 8 * tile):
+    # fused resource + top-K; unfused with scratch for one tile (span = tile) and for
+    # several tiles per top-k merge
+    for fused, scratch in ((True, 0), (False, 1), (False, 3 * U * 8 * tile)):
         v1, i1 = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile,
-                                       scratch_bytes=scratch, **kw)
-        assert torch.equal(i1, i0)
-        assert torch.equal(v1.view(torch.int64), v0.view(torch.int64))
+                                       scratch_bytes=scratch, fused=fused, **kw)
+        assert torch.equal(i1, i0), (fused, scratch)
+        assert torch.equal(v1.view(torch.int64), v0.view(torch.int64)), (fused, scratch)
 
 
 def test_spread_topk_tiled_user_shards():
@@ -219,3 +221,23 @@ def test_item_range_shards_merge_to_full(mode, world, tile):
                                   torch.stack([p[1] for p in parts]))
     assert torch.equal(mi, i0)
     assert torch.equal(mv.view(torch.int64), v0.view(torch.int64))
+
+
+@pytest.mark.parametrize("d", [32, 128])
+@pytest.mark.parametrize("k", [5, 128])
+def test_fused_dims_and_wide_k(d, k):
+    """The fused path at the other embedding widths and at k = 128 (CAP 256 lists), users
+    with fewer than k surviving columns (-1 padding), over an item sub-range."""
+    from lgcnhs import ops
+    U, I = 200, 600
+    A = _inter(U, I, 4000, seed=12, zipf=True)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
+    ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
+    for items in (None, slice(130, 470)):
+        ref = ops.spread_topk_tiled(A, 0.6, k, A.by_user, eu=eu, ei=ei, tile=128,
+                                    fused=False, scratch_bytes=1, items=items)
+        got = ops.spread_topk_tiled(A, 0.6, k, A.by_user, eu=eu, ei=ei, tile=128,
+                                    items=items, fused=True)
+        assert torch.equal(got[1], ref[1])
+        assert torch.equal(got[0].view(torch.int64), ref[0].view(torch.int64))
