@@ -107,6 +107,24 @@ def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
                       f"{e_end} directed nnz x {layers} layers, full {n}x{dim} x, median of 3"}
 
 
+def cpu_baseline_topk(e0_orig, keys, U, I, k, n_users=512):
+    """The reference's e0 scoring + -1024 masks + torch.topk (model/LightGCN/recommend.py:
+    83-114, restated by the oracle) on the host cores for a block of users x all items."""
+    from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
+    eu = e0_orig[:n_users].cpu()
+    ei = e0_orig[U:U + I].cpu()
+    blk = keys[keys < n_users * I].cpu()
+    pairs = (blk // I, blk % I)
+    O.recommend_topk_torch(eu[:8], ei, None, None, k)  # warm-up
+    t0 = time.perf_counter()
+    O.recommend_topk_torch(eu, ei, pairs, None, k)
+    secs = time.perf_counter() - t0
+    return {"value": n_users / secs, "unit": "recs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"torch.matmul + -1024 index-put + torch.topk(k={k}) for users "
+                      f"[0,{n_users}) x {I} items (fp32, the reference's op sequence)"}
+
+
 def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
     """Time `steps` full L-layer forwards; returns (max-over-ranks seconds, average SpMM
     'launch' seconds = one layer's kernels on this rank, from HIP events on the stream)."""
@@ -176,6 +194,54 @@ def bench_small_config(dev, k):
     return res
 
 
+def bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev, n_test=10_000_000):
+    """Full top-k evaluation of the C5 recommendations (metrics/accurate.py +
+    metrics/diversity.py on the device, lgcnhs.metrics): P / R / NDCG against a synthetic
+    test set (n_test random pairs outside train|val, seeded), Hamming distance over all user
+    pairs (exact closed form; the lists are all-gathered) and internal similarity over A.
+    This rank evaluates its user block; sums are all-reduced."""
+    from lgcnhs import metrics as M
+    from lgcnhs.graph import RowSets
+    g = torch.Generator(device=dev).manual_seed(11)
+    tk = torch.unique(torch.randint(0, U, (n_test,), device=dev, generator=g) * I +
+                      torch.randint(0, I, (n_test,), device=dev, generator=g))
+    pos = torch.searchsorted(keys, tk).clamp_max(keys.numel() - 1)
+    tk = tk[keys[pos] != tk]                       # test items are never train|val items
+    tk = tk[(tk >= u0 * I) & (tk < u1 * I)]        # this rank's users
+    test = RowSets.from_pairs(tk // I - u0, tk % I, u1 - u0, I, dev)
+    deg_item = A.by_item.degrees()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = M.accuracy(idx, test, k)
+    part = M.intra_similarity_parts(idx, A.by_item, deg_item)
+    sums = torch.tensor([acc["precision"] * acc["n_eval"], acc["recall"] * acc["n_eval"],
+                         acc["ndcg"] * acc["n_eval"], float(acc["n_eval"]),
+                         float(part.sum())], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(sums)
+        # every rank's lists (padded to equal blocks with -1, which match nothing)
+        nmax = -(-U // world)
+        mine = torch.full((nmax, k), -1, dtype=idx.dtype, device=dev)
+        mine[:idx.shape[0]] = idx
+        allr = torch.empty((world * nmax, k), dtype=idx.dtype, device=dev)
+        dist.all_gather_into_tensor(allr, mine)
+    else:
+        allr = idx
+    overlap = M.pair_overlap(allr, I)
+    H = (U * (U - 1) - overlap / k) / (U * (U - 1))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n = float(sums[3])
+    return {"seconds": dt, "users": U, "test_pairs_evaluated_rank0": int(tk.numel()),
+            "P": float(sums[0]) / n, "R": float(sums[1]) / n, "NDCG": float(sums[2]) / n,
+            "H": H, "I": 2.0 * float(sums[4]) / (U * k * (k - 1)),
+            "path": "lg_rec_hits + lg_rec_pair_overlap + lg_rec_intra_similarity_f64"}
+
+
 def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     """C5 LGCNHS recommendation for EVERY user (SpreadLightGCN, model/SpreadLightGCN/model.py:
     107-153 + recommend.py:18-52): per user, top-k of G * F with F = A @ HybridS(A, general_W,
@@ -203,13 +269,19 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     filled = float((idx >= 0).float().mean().item())
+    evaluation = None
+    try:
+        evaluation = bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev)
+    except Exception as ex:  # a side measurement never hides the main result
+        log(f"eval bench failed: {ex!r}")
     del A, idx
     torch.cuda.empty_cache()
     res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
            "tile": tile, "filled_frac_rank0": filled,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_tile_{seek,cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 "
-                   "(G by f32 MFMA) + lg_topk_lists_merge_f64"}
+                   "(G by f32 MFMA) + lg_topk_lists_merge_f64",
+           "eval": evaluation}
     if world == 1:
         # configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), dense
         # general_W / W (fp64 I x I), fused G * F top-k
@@ -392,10 +464,11 @@ def main():
         except Exception as ex:  # an auxiliary measurement never hides the main result
             log(f"small-config bench failed: {ex!r}")
 
-    cpu = None
+    cpu = cpu_topk = None
     if cpu_src is not None:
         try:
             cpu = cpu_baseline(cpu_rp, cpu_src, N, D, L)
+            cpu_topk = cpu_baseline_topk(e0_orig, keys, U, I, args.k)
         except Exception as ex:  # the baseline must never hide the GPU result
             log(f"cpu baseline failed: {ex!r}")
     if rank == 0:
@@ -420,6 +493,7 @@ def main():
             "other_dims": extra,
             "c2_ml1m_shape": small,
             "cpu_baseline": cpu,
+            "cpu_baseline_topk": cpu_topk,
             "host": platform.node(),
         }
         print(json.dumps(line), flush=True)
