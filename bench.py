@@ -147,12 +147,47 @@ def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t1
     kernel_ms = sum(s.elapsed_time(e) for s, e in prop.events)  # SpMM kernels only
+    comm = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        comm = time_exchange(prop, shard, D, world, dev)
     del prop, e0
-    return elapsed, kernel_ms / (steps * L) / 1e3
+    return elapsed, kernel_ms / (steps * L) / 1e3, comm
+
+
+def time_exchange(prop, shard, D, world, dev, reps=5):
+    """The all-gathers of one layer alone (no SpMM running): RCCL over xGMI, ms per layer
+    and GB/s received per GPU ((W-1)/W of the padded [n, D] fp32 table)."""
+    from lgcnhs.dist import SegmentShard, _gather_block, _gather_piece
+    buf = prop.bufs[0]
+
+    def once():
+        hs = []
+        if isinstance(shard, SegmentShard):
+            for s_, ps in enumerate(shard.seg_pieces):
+                for c in range(len(ps)):
+                    hs.append(_gather_piece(buf, shard, s_, c, prop.group))
+        else:
+            for c in range(shard.chunks):
+                hs.append(_gather_block(buf, shard, c, prop.group))
+        for h in hs:
+            h.wait()
+    once()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    t = torch.tensor([dt], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    recv = (world - 1) / world * shard.n_pad * D * 4
+    return {"allgather_ms_per_layer": dt * 1e3, "recv_GBps_per_gpu": recv / dt / 1e9,
+            "recv_bytes_per_gpu": recv}
 
 
 def bench_small_config(dev, k):
@@ -260,10 +295,17 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    st = {}  # W entries gathered by the resource passes (= path updates of F = A W)
     (u0, u1), _, idx = sharded_spread_topk(A, lam, k, A.by_user, True, eu, ei, rank=rank,
-                                           world=world, tile=tile, scratch_bytes=32 << 30)
+                                           world=world, tile=tile, scratch_bytes=32 << 30,
+                                           stats=st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    entries = float(st.get("w_entries_read", 0))
+    if world > 1:
+        e = torch.tensor([entries], dtype=torch.float64, device=dev)
+        dist.all_reduce(e)
+        entries = float(e.item())
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -277,6 +319,8 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     del A, idx
     torch.cuda.empty_cache()
     res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
+           "path_updates_per_s": entries / dt,
+           "w_entry_GBps": entries * 12 / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_tile_{seek,cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 "
@@ -397,8 +441,8 @@ def main():
     log(f"[rank {rank}] graph U={U} I={I} nnz={nnz} rows {getattr(shard, 'ranges', None) or (shard.g0, shard.g1)} "
         f"setup {time.time() - t0:.1f}s")
 
-    elapsed, avg_kernel_s = time_propagation(shard, dis_l, e0_orig, D, L, args.steps,
-                                             args.warmup, world, dev)
+    elapsed, avg_kernel_s, comm = time_propagation(shard, dis_l, e0_orig, D, L, args.steps,
+                                                   args.warmup, world, dev)
     edge_layers = nnz * L * args.steps
     value = edge_layers / elapsed
     # algorithmic bytes per SpMM launch: nnz*(8+4d) + rows*(4+4d)
@@ -412,8 +456,8 @@ def main():
         if d2 == D:
             continue
         e2 = torch.randn(N, d2, device=dev, generator=gen) * 0.1
-        el2, k2 = time_propagation(shard, dis_l, e2, d2, L, max(2, args.steps // 2), 1, world,
-                                   dev)
+        el2, k2, _ = time_propagation(shard, dis_l, e2, d2, L, max(2, args.steps // 2), 1,
+                                      world, dev)
         b2 = shard.nnz * (8 + 4 * d2) + shard.n_rows * (4 + 4 * d2)
         extra[f"d{d2}"] = {"value": nnz * L * max(2, args.steps // 2) / el2,
                            "unit": "edge-layers/s", "ms_per_step": el2 / max(2, args.steps // 2) * 1e3,
@@ -488,6 +532,7 @@ def main():
                          "traffic": traffic, "kernel": "lg_spmm_layer_f32",
                          "avg_launch_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes},
+            "comm": comm,
             "topk": topk,
             "spread": spread,
             "other_dims": extra,

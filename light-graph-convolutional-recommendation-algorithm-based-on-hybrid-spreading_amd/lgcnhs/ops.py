@@ -403,6 +403,8 @@ class TileWeights:
             N.ptr(self.meta), N.ptr(self.ws), self.ws.numel(), strm),
             "lg_spread_tile_weight_f64")
         self.j0, self.width = j0, width
+        if getattr(self, "row_uses", None) is not None:
+            self.entries_read += (self.row_uses * (self.meta >> 48)).sum()
 
     def resource(self, u0: int, u1: int, out: torch.Tensor) -> torch.Tensor:
         """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
@@ -434,7 +436,8 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       drop: bool = True, eu: torch.Tensor | None = None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
                       tile: int = 2048, scratch_bytes: int = 4 << 30,
-                      items: slice | None = None, fused: bool | None = None):
+                      items: slice | None = None, fused: bool | None = None,
+                      stats: dict | None = None):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). Bitwise the result of
     spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
@@ -450,7 +453,9 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     default without a G factor; with one (SpreadLightGCN), the score of every surviving
     column must be computed per user from global item rows, which costs more than the F
     round trip (C5: 14.4 s fused vs 8.1 s with the 16-user MFMA tiles of lg_tile_topk_f64),
-    so the default there is the two-kernel path."""
+    so the default there is the two-kernel path. ``stats`` (optional dict) receives
+    "w_entries_read": the W entries the resource pass gathers, sum over tiles and users u of
+    sum_{i in items(u)} |row i of W in the tile| (= the path updates of F = A W)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -468,8 +473,15 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     eu_r = None if eu is None else eu[u0:u1]
     if fused is None:
         fused = eu is None
+    if stats is not None:
+        # users of each item among [u0, u1): the times its W row is gathered per tile
+        cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
+        tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
+        tw.entries_read = torch.zeros((), dtype=torch.int64, device=dev)
     if fused:
         _fused_walk(A, tw, u0, u1, i0, i1, k, ex if drop else None, eu_r, ei, vals, idxs)
+        if stats is not None:
+            stats["w_entries_read"] = stats.get("w_entries_read", 0) + int(tw.entries_read)
         return vals, idxs
     span = max(tile, scratch_bytes // (n * 8) // tile * tile)
     span = min(span, -(-(i1 - i0) // tile) * tile)
@@ -480,6 +492,8 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
             tw.build(j0, stop=i1)
             tw.resource(u0, u1, F[:, j0 - s0:])
         tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
+    if stats is not None:
+        stats["w_entries_read"] = stats.get("w_entries_read", 0) + int(tw.entries_read)
     return vals, idxs
 
 

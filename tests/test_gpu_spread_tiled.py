@@ -241,3 +241,25 @@ def test_fused_dims_and_wide_k(d, k):
                                     items=items, fused=True)
         assert torch.equal(got[1], ref[1])
         assert torch.equal(got[0].view(torch.int64), ref[0].view(torch.int64))
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_spread_stats_count_path_updates(fused):
+    """stats["w_entries_read"] = sum over the users' items of the W row lengths inside the
+    item range = the nonzero path updates of F = A W (dense general_W nonzeros)."""
+    from lgcnhs import ops
+    U, I = 150, 400
+    A = _inter(U, I, 3000, seed=3, zipf=True)
+    gW = ops.spread_general(A).cpu().numpy()
+    deg_rows = (gW != 0)
+    Ad = np.zeros((U, I))
+    rp, col = A.by_user.rowptr.cpu().numpy(), A.by_user.col.cpu().numpy()
+    for u in range(U):
+        Ad[u, col[rp[u]:rp[u + 1]]] = 1
+    for users, items in ((slice(0, U), slice(0, I)), (slice(20, 90), slice(77, 301))):
+        st = {}
+        ops.spread_topk_tiled(A, 0.5, 10, A.by_user, tile=64, users=users, items=items,
+                              fused=fused, stats=st)
+        uses = Ad[users].sum(0)
+        want = int((uses[:, None] * deg_rows[:, items]).sum())
+        assert st["w_entries_read"] == want
