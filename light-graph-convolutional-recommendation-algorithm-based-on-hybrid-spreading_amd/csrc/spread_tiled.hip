@@ -308,18 +308,69 @@ __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ wt
   if (wt_ptr[i + 1] - wt_ptr[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
 }
 
-// F[u][j - j0] = sum over items(u) ascending of W[i][j]; one wave per user, the tile's
-// accumulator in LDS (tile doubles per wave) plus a 128-row index (LDS, 1.5 KiB per wave).
-// Rows are taken 128 at a time: their metadata is fetched in one round trip (two loads per
-// lane), then their entries are flattened: lane l takes entries e = e0 + q*64 + l of the
-// concatenated rows (its row found by a binary search over the rows' inclusive length
-// prefix in LDS), so each load instruction moves 64 useful 12-byte entries whatever the row
-// lengths, UF of them in flight per lane. Entries go in with ds_add_f64; entries of one
-// instruction that hit the same column come from rows in lane order, and rows are
-// flattened in ascending order, so each column still receives its rows' values in
-// ascending row order (the order of lg_spread_resource_f64).
+// Resource pass (F = A W over one tile): rows of 128 items per group, see k_tile_resource.
 constexpr int kResRows = 128;
 constexpr int kResIdxBytes = kResRows * (4 + 8);
+
+// Prefix of a 128-row group's metadata (rows' entry counts and starts) into the wave's
+// row index `idx`; returns the group's total entry count.
+__device__ __forceinline__ int write_row_index(char *idx, uint64_t m0, uint64_t m1) {
+  const int lane = lane_id();
+  int64_t *s_base = reinterpret_cast<int64_t *>(idx);
+  int *s_incl = reinterpret_cast<int *>(idx + kResRows * 8);
+  const int rl0 = (int)(m0 >> kMetaShift), rl1 = (int)(m1 >> kMetaShift);
+  int in0 = rl0, in1 = rl1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y0 = __shfl_up(in0, o), y1 = __shfl_up(in1, o);
+    if (lane >= o) { in0 += y0; in1 += y1; }
+  }
+  in1 += __shfl(in0, 63);
+  const int total = __shfl(in1, 63);
+  wave_sync();  // earlier readers of this index are done
+  s_incl[lane] = in0;
+  s_incl[64 + lane] = in1;
+  s_base[lane] = (int64_t)(m0 & kMetaPtrMask) - (in0 - rl0);
+  s_base[64 + lane] = (int64_t)(m1 & kMetaPtrMask) - (in1 - rl1);
+  wave_sync();
+  return total;
+}
+
+// acc[j - item_begin] += the `total` flattened entries of one indexed row group.
+template <int UF>
+__device__ __forceinline__ void accumulate_group(double *acc, const char *idx, int total,
+                                                 const WEnt *__restrict__ wt_ent,
+                                                 int32_t item_begin) {
+  const int lane = lane_id();
+  const int64_t *s_base = reinterpret_cast<const int64_t *>(idx);
+  const int *s_incl = reinterpret_cast<const int *>(idx + kResRows * 8);
+  for (int e0 = 0; e0 < total; e0 += 64 * UF) {
+    // r[q] = number of rows whose inclusive end is <= e[q] (the row holding entry e[q]):
+    // the UF binary searches advance in lockstep (independent LDS reads per step, no
+    // branch), then the UF entry loads issue back to back. Lanes past the end re-read
+    // the last entry and skip the add.
+    int e[UF], r[UF];
+#pragma unroll
+    for (int q = 0; q < UF; ++q) {
+      const int x = e0 + q * 64 + lane;
+      e[q] = x < total ? x : total - 1;
+      r[q] = 0;
+    }
+#pragma unroll
+    for (int st = 64; st > 0; st >>= 1)
+#pragma unroll
+      for (int q = 0; q < UF; ++q) r[q] += s_incl[r[q] + st - 1] <= e[q] ? st : 0;
+    WEnt w[UF];
+#pragma unroll
+    for (int q = 0; q < UF; ++q) w[q] = wt_ent[s_base[r[q]] + e[q]];
+#pragma unroll
+    for (int q = 0; q < UF; ++q)
+      if (e0 + q * 64 + lane < total)
+        __hip_atomic_fetch_add(&acc[w[q].col - item_begin],
+                               __hiloint2double((int)w[q].hi, (int)w[q].lo), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
 
 // acc[j - item_begin] += W[i][j] for every item i of user u (ascending), acc = the wave's
 // LDS tile accumulator (zeroed by the caller), idx = its kResIdxBytes row index.
@@ -332,8 +383,6 @@ __device__ __forceinline__ void accumulate_user_tile(double *acc, char *idx,
                                                      const WEnt *__restrict__ wt_ent,
                                                      int32_t item_begin) {
   const int lane = lane_id();
-  int64_t *s_base = reinterpret_cast<int64_t *>(idx);               // entry e of row r: base_r + e
-  int *s_incl = reinterpret_cast<int *>(idx + kResRows * 8);         // inclusive entry prefix
   const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
   for (int64_t p0 = pb; p0 < pe; p0 += kResRows) {
     uint64_t m0 = 0, m1 = 0;
@@ -343,54 +392,31 @@ __device__ __forceinline__ void accumulate_user_tile(double *acc, char *idx,
       if (i0 >= 0) m0 = wt_meta[i0];
       if (i1 >= 0) m1 = wt_meta[i1];
     }
-    const int rl0 = (int)(m0 >> kMetaShift), rl1 = (int)(m1 >> kMetaShift);
-    int in0 = rl0, in1 = rl1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y0 = __shfl_up(in0, o), y1 = __shfl_up(in1, o);
-      if (lane >= o) { in0 += y0; in1 += y1; }
-    }
-    const int t0 = __shfl(in0, 63);
-    in1 += t0;
-    const int total = __shfl(in1, 63);
-    wave_sync();  // the previous group's readers of the index are done
-    s_incl[lane] = in0;
-    s_incl[64 + lane] = in1;
-    s_base[lane] = (int64_t)(m0 & kMetaPtrMask) - (in0 - rl0);
-    s_base[64 + lane] = (int64_t)(m1 & kMetaPtrMask) - (in1 - rl1);
-    wave_sync();
-    for (int e0 = 0; e0 < total; e0 += 64 * UF) {
-      // r[q] = number of rows whose inclusive end is <= e[q] (the row holding entry e[q]):
-      // the UF binary searches advance in lockstep (independent LDS reads per step, no
-      // branch), then the UF entry loads issue back to back. Lanes past the end re-read
-      // the last entry and skip the add.
-      int e[UF], r[UF];
-#pragma unroll
-      for (int q = 0; q < UF; ++q) {
-        const int x = e0 + q * 64 + lane;
-        e[q] = x < total ? x : total - 1;
-        r[q] = 0;
-      }
-#pragma unroll
-      for (int st = 64; st > 0; st >>= 1)
-#pragma unroll
-        for (int q = 0; q < UF; ++q) r[q] += s_incl[r[q] + st - 1] <= e[q] ? st : 0;
-      WEnt w[UF];
-#pragma unroll
-      for (int q = 0; q < UF; ++q) w[q] = wt_ent[s_base[r[q]] + e[q]];
-#pragma unroll
-      for (int q = 0; q < UF; ++q)
-        if (e0 + q * 64 + lane < total)
-          __hip_atomic_fetch_add(&acc[w[q].col - item_begin],
-                                 __hiloint2double((int)w[q].hi, (int)w[q].lo),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    const int total = write_row_index(idx, m0, m1);
+    accumulate_group<UF>(acc, idx, total, wt_ent, item_begin);
   }
   wave_sync();
 }
 
+// F[u][j - j0] = sum over items(u) ascending of W[i][j]; the tile's accumulator in LDS (tile
+// doubles per wave) plus two 128-row indexes (LDS, 1.5 KiB each). Rows are taken 128 at a
+// time: their metadata is fetched in one round trip (two loads per lane), then their entries
+// are flattened: lane l takes entries e = e0 + q*64 + l of the concatenated rows (its row
+// found by a binary search over the rows' inclusive length prefix in LDS), so each load
+// instruction moves 64 useful 12-byte entries whatever the row lengths, UF of them in flight
+// per lane. Entries go in with ds_add_f64; entries of one instruction that hit the same
+// column come from rows in lane order, and rows are flattened in ascending order, so each
+// column still receives its rows' values in ascending row order (the order of
+// lg_spread_resource_f64).
+//
+// Persistent waves, software-pipelined over the users u, u+G, u+2G, ... of a wave (G = waves
+// in the grid): a user's chain is row pointers -> item ids -> row metadata -> entries, four
+// dependent memory round trips. While user u's entries are in flight the wave also has in
+// flight the metadata of u+G, the item ids of u+2G and the row pointers of u+3G, so each user
+// costs about one round trip (the first group of 128 items; longer rows add their groups
+// unpipelined).
 template <int UF>
-__global__ __launch_bounds__(256) void k_tile_resource(
+__global__ __launch_bounds__(128) void k_tile_resource(
     const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
     int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
     int32_t item_begin, int32_t tile, double *__restrict__ F, int64_t ldf) {
@@ -398,14 +424,77 @@ __global__ __launch_bounds__(256) void k_tile_resource(
   const int wave = threadIdx.x / 64;
   const int wpb = blockDim.x / 64;
   const int lane = lane_id();
-  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
+  const int64_t G = (int64_t)gridDim.x * wpb;
+  int64_t u = (int64_t)blockIdx.x * wpb + wave;
   if (u >= n_users) return;
-  double *acc = lds + (int64_t)wave * tile;
-  char *idx = reinterpret_cast<char *>(lds + (int64_t)wpb * tile) + wave * kResIdxBytes;
+  double *acc = lds + (int64_t)wave * (tile + 2 * kResIdxBytes / 8);
+  char *idx0 = reinterpret_cast<char *>(acc + tile);
+  char *idx1 = idx0 + kResIdxBytes;
   for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
-  accumulate_user_tile<UF>(acc, idx, user_rowptr, user_items, u, wt_meta, wt_ent, item_begin);
-  double *row = F + u * ldf;
-  for (int j = lane; j < tile; j += 64) row[j] = acc[j];
+
+  auto rows = [&](int64_t v, int64_t &b, int64_t &e) __attribute__((always_inline)) {
+    b = e = 0;
+    if (v < n_users) {
+      b = user_rowptr[v];
+      e = user_rowptr[v + 1];
+    }
+  };
+  auto items = [&](int64_t b, int64_t e, int32_t &i0, int32_t &i1) __attribute__((always_inline)) {
+    i0 = b + lane < e ? user_items[b + lane] : -1;
+    i1 = b + 64 + lane < e ? user_items[b + 64 + lane] : -1;
+  };
+  auto meta = [&](int32_t i0, int32_t i1, uint64_t &m0, uint64_t &m1) __attribute__((always_inline)) {
+    m0 = i0 >= 0 ? wt_meta[i0] : 0;
+    m1 = i1 >= 0 ? wt_meta[i1] : 0;
+  };
+
+  // prologue: user u indexed; u+G's item ids and u+2G's row pointers loaded
+  int64_t b0, e0, b1, e1, b2, e2;
+  rows(u, b0, e0);
+  rows(u + G, b1, e1);
+  rows(u + 2 * G, b2, e2);
+  int32_t ia, ib, ja, jb;
+  items(b0, e0, ia, ib);
+  items(b1, e1, ja, jb);
+  uint64_t ma, mb;
+  meta(ia, ib, ma, mb);
+  char *cur = idx0, *nxt = idx1;
+  int total = write_row_index(cur, ma, mb);
+  for (;;) {
+    int32_t ka, kb;
+    items(b2, e2, ka, kb);           // u+2G
+    uint64_t na, nb;
+    meta(ja, jb, na, nb);            // u+G
+    int64_t b3, e3;
+    rows(u + 3 * G, b3, e3);         // u+3G
+    accumulate_group<UF>(acc, cur, total, wt_ent, item_begin);
+    for (int64_t p0 = b0 + kResRows; p0 < e0; p0 += kResRows) {  // rows beyond 128 items
+      int32_t xa, xb;
+      items(p0, e0, xa, xb);
+      uint64_t ya, yb;
+      meta(xa, xb, ya, yb);
+      const int t2 = write_row_index(cur, ya, yb);
+      accumulate_group<UF>(acc, cur, t2, wt_ent, item_begin);
+    }
+    wave_sync();
+    const bool more = u + G < n_users;
+    if (more) total = write_row_index(nxt, na, nb);
+    double *row = F + u * ldf;
+    for (int j = lane; j < tile; j += 64) {
+      row[j] = acc[j];
+      acc[j] = 0.0;
+    }
+    wave_sync();  // zeroes land before the next user's adds
+    if (!more) break;
+    u += G;
+    char *t = cur;
+    cur = nxt;
+    nxt = t;
+    b0 = b1; e0 = e1;
+    b1 = b2; e1 = e2;
+    b2 = b3; e2 = e3;
+    ja = ka; jb = kb;
+  }
 }
 
 template <int Q>
@@ -1009,13 +1098,24 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
   LG_REQUIRE(tile >= 1 && tile <= 8192, "lg_spread_tile_resource_f64: tile %d not in [1, 8192]",
              tile);
   if (n_users == 0) return LG_OK;
-  // tile doubles of LDS per wave (<= 64 KiB at tile 8192); small blocks so the CU's LDS
-  // holds as many waves as it can
-  const int waves = tile <= 1024 ? 4 : (tile <= 2048 ? 2 : 1);
-  const size_t lds = (size_t)waves * (tile * sizeof(double) + kResIdxBytes);
-  k_tile_resource<16><<<dim3((unsigned)((n_users + waves - 1) / waves)), dim3(64 * waves), lds,
-                       (hipStream_t)stream>>>(user_rowptr, user_items, n_users, wt_meta,
-                                              (const WEnt *)wt_ent, item_begin, tile, F, ldf);
+  // per wave: tile doubles + two row indexes; 2-wave blocks, as many resident per CU as the
+  // LDS holds, and a persistent grid of exactly that many (each wave walks users u + k*G)
+  const size_t per_wave = (size_t)tile * sizeof(double) + 2 * kResIdxBytes;
+  const size_t lds = 2 * per_wave;
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+      n_cu = 256;
+  }
+  const int64_t per_cu = (int64_t)(160 * 1024 / lds) > 0 ? (int64_t)(160 * 1024 / lds) : 1;
+  const int64_t want = (n_users + 1) / 2;
+  const int64_t cap = per_cu * n_cu;
+  const unsigned blocks = (unsigned)(want < cap ? want : cap);
+  k_tile_resource<16><<<dim3(blocks), dim3(128), lds, (hipStream_t)stream>>>(
+      user_rowptr, user_items, n_users, wt_meta, (const WEnt *)wt_ent, item_begin, tile, F, ldf);
   return launch_status("lg_spread_tile_resource_f64");
 }
 

@@ -263,3 +263,39 @@ def test_spread_stats_count_path_updates(fused):
         uses = Ad[users].sum(0)
         want = int((uses[:, None] * deg_rows[:, items]).sum())
         assert st["w_entries_read"] == want
+
+
+@pytest.mark.parametrize("zipf", [False, True])
+def test_tile_resource_persistent_waves_bitwise(zipf):
+    """More users than resident waves (each persistent wave walks several users with the
+    next users' rows / items / metadata prefetched), users with no items and users with
+    more than 128 items (unpipelined extra groups): every F tile equals the dense F."""
+    from lgcnhs import ops
+    from lgcnhs.synth import synth_interactions
+    U, I = 6000, 300
+    u, i = synth_interactions(U, I, 60000 if zipf else 30000, seed=21,
+                              dist="zipf" if zipf else "uniform")
+    keep = (u % 997) != 5                     # a few users with no items at all
+    u, i = u[keep], i[keep]
+    heavy = np.repeat(np.arange(3, 3000, 500), 200)
+    hi = np.tile(np.arange(200) + 50, heavy.size // 200)
+    u, i = np.concatenate([u, heavy]), np.concatenate([i, hi])
+    A = ops.Interactions.from_pairs(torch.as_tensor(u), torch.as_tensor(i), U, I, DEV)
+    assert int(A.by_user.degrees().max()) > 128 and int((A.by_user.degrees() == 0).sum()) > 0
+    W = ops.hybrid_weight(ops.spread_general(A), A.k_item, 0.5)
+    F = ops.spread_resource(A, W).cpu().numpy()
+    tile = 128
+    tw = ops.TileWeights(A, 0.5, tile)
+    Fb = torch.empty((U, tile), dtype=torch.float64, device=DEV)
+    for j0 in range(0, I, tile):
+        tw.build(j0)
+        tw.resource(0, U, Fb)
+        Ft = Fb[:, :tw.width].cpu().numpy()
+        assert np.array_equal(Ft.view(np.uint64), F[:, j0:j0 + tw.width].view(np.uint64))
+    # a user sub-range (the resource pass of a user block)
+    Fb2 = torch.empty((2500, tile), dtype=torch.float64, device=DEV)
+    tw2 = ops.TileWeights(A, 0.5, tile)
+    tw2.build(0)
+    tw2.resource(1000, 3500, Fb2)
+    assert np.array_equal(Fb2[:, :tw2.width].cpu().numpy().view(np.uint64),
+                          F[1000:3500, :tw2.width].view(np.uint64))
