@@ -53,13 +53,20 @@ def exclusion_from_dfs(user_num: int, item_num: int, *dfs: pd.DataFrame, device=
     return RowSets.from_pairs(u, i, user_num, item_num, dev)
 
 
-def topk_to_dict(idx: torch.Tensor) -> dict:
-    """[U, k] indices (-1 = padding) -> {uid: [item, ...]}."""
+def topk_to_dict(idx: torch.Tensor, n_rows: int | None = None, factory=dict) -> dict:
+    """[U, k] indices (-1 = trailing padding) -> {uid: [item, ...]} with one device->host
+    copy and one tolist(); only rows that are padded get trimmed (the
+    reference builds these dicts per user and per item in Python)."""
     a = idx.cpu().numpy()
-    out = {}
-    for u in range(a.shape[0]):
-        row = a[u]
-        out[u] = row[row >= 0].tolist()
+    if n_rows is not None:
+        a = a[:n_rows]
+    rows = a.tolist()
+    if a.size:
+        counts = (a >= 0).sum(1)
+        for u in np.nonzero(counts < a.shape[1])[0].tolist():
+            rows[u] = rows[u][:counts[u]]
+    out = factory()
+    out.update(enumerate(rows))
     return out
 
 

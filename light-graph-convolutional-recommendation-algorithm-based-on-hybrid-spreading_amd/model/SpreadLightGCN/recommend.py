@@ -13,16 +13,11 @@ import torch
 
 from const import cfg
 from lgcnhs import ops
-from lgcnhs.recs import exclusion_from_dfs, gpu_device, save_recs
+from lgcnhs.recs import topk_to_dict, exclusion_from_dfs, gpu_device, save_recs
 
 
 def _to_dict(idx: torch.Tensor, user_num: int) -> dict:
-    a = idx.cpu().numpy()
-    recs = defaultdict(list)
-    for u in range(user_num):
-        row = a[u]
-        recs[u] = row[row >= 0].tolist()
-    return recs
+    return topk_to_dict(idx, user_num, defaultdict)
 
 
 def _save(recs: dict) -> None:

@@ -1,0 +1,29 @@
+"""Host-side glue on CPU (no kernels): the [U, k] -> dict conversion of the recommend
+modules (reference model/*/recommend.py dict building)."""
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+
+def test_topk_to_dict_trims_padding_and_keeps_order():
+    from lgcnhs.recs import topk_to_dict
+    idx = torch.tensor([[5, 3, 9], [7, -1, -1], [-1, -1, -1], [0, 1, 2]])
+    d = topk_to_dict(idx)
+    assert d == {0: [5, 3, 9], 1: [7], 2: [], 3: [0, 1, 2]}
+    assert all(type(x) is int for v in d.values() for x in v)
+    d2 = topk_to_dict(idx, n_rows=2, factory=defaultdict)
+    assert isinstance(d2, defaultdict) and dict(d2) == {0: [5, 3, 9], 1: [7]}
+    assert topk_to_dict(torch.zeros((0, 4), dtype=torch.int64)) == {}
+
+
+def test_topk_to_dict_large_matches_loop():
+    from lgcnhs.recs import topk_to_dict
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 1000, size=(5000, 20))
+    pad = rng.integers(0, 21, size=5000)
+    for u in range(5000):
+        a[u, pad[u]:] = -1
+    d = topk_to_dict(torch.as_tensor(a))
+    for u in range(5000):
+        assert d[u] == a[u][a[u] >= 0].tolist()
