@@ -399,7 +399,12 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # RCCL on a high-priority stream: its all-gather workgroups are dispatched ahead
+            # of the queued SpMM workgroups they overlap with
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    pg_options=opts)
         else:
             dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
