@@ -28,6 +28,8 @@
 //            (G = e0 score by f32 MFMA, the chain of lg_score_topk_f32, promoted to fp64).
 // Work: the weight pass costs sum_i deg(i) lookups + the 2-hop pairs once per tile (not per
 // user); the resource pass reads deg(u) short row segments per user and tile.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace lg {
@@ -513,7 +515,7 @@ __device__ __forceinline__ void load_frag(const float *__restrict__ p, float (&v
 // Merge the tile's columns of (G *) F into running per-user top-K lists (io_val/io_idx,
 // sorted, index -1 = empty). D = 0: no G factor. One wave = NG groups of 16 users (rows);
 // lane (ul, gq) holds user ul of each group and items 4gq..4gq+3 of each 16-item step.
-template <int D, int NG, int M>
+template <int D, int NG, int M, bool VEC>
 __global__ __launch_bounds__(128) void k_tile_topk(
     const double *__restrict__ F, int64_t ldf, int64_t n_rows, int32_t item_begin,
     int32_t n_cols, const float *__restrict__ eu, const float *__restrict__ ei,
@@ -625,6 +627,10 @@ __global__ __launch_bounds__(128) void k_tile_topk(
 
   // One 16-column step: the item fragment and the F values (clamped to valid memory, so
   // every step issues the same loads) are loaded one step ahead.
+  // VEC: ldf >= n_cols rounded up to 16, so a step's 16 columns are always inside the row:
+  // the step start is clamped to the last step and each lane reads its 4 columns as two
+  // 16-byte loads (columns past n_cols are never inserted: process() checks c < n_cols).
+  const int last_step = ((n_cols - 1) / 16) * 16;
   auto load_step = [&](int it, float(&af)[Q], double(&f)[NG][4]) __attribute__((always_inline)) {
     if constexpr (D > 0) {
       const int jc = it + ul < n_cols ? item_begin + it + ul : item_begin + n_cols - 1;
@@ -634,10 +640,20 @@ __global__ __launch_bounds__(128) void k_tile_topk(
     for (int g = 0; g < NG; ++g) {
       const int64_t row = ubase + g * 16 + ul;
       const double *fr = F + (row < n_rows ? row : n_rows - 1) * ldf;
+      if constexpr (VEC) {
+        const int c0 = (it < last_step ? it : last_step) + gq * 4;
+        const double2 a = *reinterpret_cast<const double2 *>(fr + c0);
+        const double2 b = *reinterpret_cast<const double2 *>(fr + c0 + 2);
+        f[g][0] = a.x;
+        f[g][1] = a.y;
+        f[g][2] = b.x;
+        f[g][3] = b.y;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = it + gq * 4 + r;
-        f[g][r] = fr[c < n_cols ? c : n_cols - 1];
+        for (int r = 0; r < 4; ++r) {
+          const int c = it + gq * 4 + r;
+          f[g][r] = fr[c < n_cols ? c : n_cols - 1];
+        }
       }
     }
   };
@@ -896,26 +912,42 @@ __global__ __launch_bounds__(128) void k_tile_resource_topk(
   }
 }
 
+template <int D, bool VEC>
+static void launch_tile_topk_v(int M, const double *F, int64_t ldf, int64_t n_rows, int32_t j0,
+                               int32_t n_cols, const float *eu, const float *ei,
+                               const int64_t *ex_rowptr, const int32_t *ex_col, int drop,
+                               int k, int first, double *io_val, int64_t *io_idx,
+                               hipStream_t s) {
+  // LDS per block (2 waves): 2 * NG * 16 * CAP * 12 B = 48 KiB (M=1, NG=2), 48 KiB (M=2,
+  // NG=1), 96 KiB (M=4, NG=1)
+  if (M == 1) {
+    const unsigned b = (unsigned)((n_rows + 63) / 64);
+    k_tile_topk<D, 2, 1, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  } else if (M == 2) {
+    const unsigned b = (unsigned)((n_rows + 31) / 32);
+    k_tile_topk<D, 1, 2, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  } else {
+    const unsigned b = (unsigned)((n_rows + 31) / 32);
+    k_tile_topk<D, 1, 4, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  }
+}
+
 template <int D>
 static void launch_tile_topk(int M, const double *F, int64_t ldf, int64_t n_rows, int32_t j0,
                              int32_t n_cols, const float *eu, const float *ei,
                              const int64_t *ex_rowptr, const int32_t *ex_col, int drop, int k,
                              int first, double *io_val, int64_t *io_idx, hipStream_t s) {
-  // LDS per block (2 waves): 2 * NG * 16 * CAP * 12 B = 48 KiB (M=1, NG=2), 48 KiB (M=2,
-  // NG=1), 96 KiB (M=4, NG=1)
-  if (M == 1) {
-    const unsigned b = (unsigned)((n_rows + 63) / 64);
-    k_tile_topk<D, 2, 1><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
-  } else if (M == 2) {
-    const unsigned b = (unsigned)((n_rows + 31) / 32);
-    k_tile_topk<D, 1, 2><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
-  } else {
-    const unsigned b = (unsigned)((n_rows + 31) / 32);
-    k_tile_topk<D, 1, 4><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
-  }
+  const bool vec = ldf >= ((int64_t)n_cols + 15) / 16 * 16 && (ldf % 2) == 0 &&
+                   ((uintptr_t)F % 16) == 0;
+  if (vec)
+    launch_tile_topk_v<D, true>(M, F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr, ex_col, drop,
+                                k, first, io_val, io_idx, s);
+  else
+    launch_tile_topk_v<D, false>(M, F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr, ex_col,
+                                 drop, k, first, io_val, io_idx, s);
 }
 
 // Merge n_lists sorted top-K lists per row ([n_lists][n_rows][k], index -1 = empty) into one
@@ -1110,9 +1142,16 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
         n_cu <= 0)
       n_cu = 256;
   }
+  // LGCNHS_RES_BLOCKS_PER_CU (A/B knob): resident-block multiple of the persistent grid;
+  // 0 = one wave per user (no persistence)
+  static int mult = -1;
+  if (mult < 0) {
+    const char *e = getenv("LGCNHS_RES_BLOCKS_PER_CU");
+    mult = e ? atoi(e) : 0;
+  }
   const int64_t per_cu = (int64_t)(160 * 1024 / lds) > 0 ? (int64_t)(160 * 1024 / lds) : 1;
   const int64_t want = (n_users + 1) / 2;
-  const int64_t cap = per_cu * n_cu;
+  const int64_t cap = mult > 0 ? per_cu * n_cu * mult : want;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   k_tile_resource<16><<<dim3(blocks), dim3(128), lds, (hipStream_t)stream>>>(
       user_rowptr, user_items, n_users, wt_meta, (const WEnt *)wt_ent, item_begin, tile, F, ldf);
