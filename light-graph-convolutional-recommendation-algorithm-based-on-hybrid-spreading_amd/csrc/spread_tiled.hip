@@ -920,7 +920,18 @@ static void launch_tile_topk_v(int M, const double *F, int64_t ldf, int64_t n_ro
                                hipStream_t s) {
   // LDS per block (2 waves): 2 * NG * 16 * CAP * 12 B = 48 KiB (M=1, NG=2), 48 KiB (M=2,
   // NG=1), 96 KiB (M=4, NG=1)
-  if (M == 1) {
+  // LGCNHS_TILE_TOPK_NG1 (A/B knob): one 16-user group per wave at k <= 32 (24 KiB blocks,
+  // twice the waves per CU, one MFMA chain per wave)
+  static int ng1 = -1;
+  if (ng1 < 0) {
+    const char *e = getenv("LGCNHS_TILE_TOPK_NG1");
+    ng1 = e ? atoi(e) : 0;
+  }
+  if (M == 1 && ng1) {
+    const unsigned b = (unsigned)((n_rows + 31) / 32);
+    k_tile_topk<D, 1, 1, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
+                                            ex_col, drop, k, first, io_val, io_idx);
+  } else if (M == 1) {
     const unsigned b = (unsigned)((n_rows + 63) / 64);
     k_tile_topk<D, 2, 1, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
                                             ex_col, drop, k, first, io_val, io_idx);
