@@ -125,6 +125,34 @@ def cpu_baseline_topk(e0_orig, keys, U, I, k, n_users=512):
                       f"[0,{n_users}) x {I} items (fp32, the reference's op sequence)"}
 
 
+def cpu_baseline_spread(k, lam=0.5):
+    """The reference's dense SpreadLightGCN op sequence (model/SpreadMethod/model.py:14-99,
+    model/SpreadLightGCN/model.py:140-151, recommend.py:18-52; restated by the oracle in
+    numpy fp64) on the host cores, at the Douban-shaped stand-in the GPU's c3_douban_shape
+    line times: general_W, HybridS, F = A W, G (fp32 e0 scores) * F, filtered top-k."""
+    import numpy as np
+    from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
+    from lgcnhs.synth import synth_interactions
+    du, di, de = 600, 20_000, 60_000
+    users, items = synth_interactions(du, di, de, seed=3, dist="zipf")
+    g = torch.Generator().manual_seed(42)
+    eu = torch.randn(du, 64, generator=g) * 0.1
+    ei = torch.randn(di, 64, generator=g) * 0.1
+    t0 = time.perf_counter()
+    A = O.interaction_matrix(du, di, users, items)
+    W = O.hybrid_s(A, O.spreading_general_mat(A), lam)
+    F = O.get_resource(A, W)
+    del W
+    F = torch.matmul(eu, ei.T).numpy() * F
+    rp = np.searchsorted(users, np.arange(du + 1))
+    O.rows_topk(F, k, rp, items.astype(np.int32), True)
+    secs = time.perf_counter() - t0
+    return {"value": du / secs, "unit": "recs/s", "cores": torch.get_num_threads(),
+            "kind": "port", "seconds": secs,
+            "sample": f"dense fp64 numpy general_W / HybridS / A@W, G*F, filtered top-{k}: "
+                      f"{du} users x {di} items, {de} Zipf interactions (c3_douban_shape)"}
+
+
 def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
     """Time `steps` full L-layer forwards; returns (max-over-ranks seconds, average SpMM
     'launch' seconds = one layer's kernels on this rank, from HIP events on the stream)."""
@@ -513,11 +541,12 @@ def main():
         except Exception as ex:  # an auxiliary measurement never hides the main result
             log(f"small-config bench failed: {ex!r}")
 
-    cpu = cpu_topk = None
+    cpu = cpu_topk = cpu_spread = None
     if cpu_src is not None:
         try:
             cpu = cpu_baseline(cpu_rp, cpu_src, N, D, L)
             cpu_topk = cpu_baseline_topk(e0_orig, keys, U, I, args.k)
+            cpu_spread = cpu_baseline_spread(args.k)
         except Exception as ex:  # the baseline must never hide the GPU result
             log(f"cpu baseline failed: {ex!r}")
     if rank == 0:
@@ -544,6 +573,7 @@ def main():
             "c2_ml1m_shape": small,
             "cpu_baseline": cpu,
             "cpu_baseline_topk": cpu_topk,
+            "cpu_baseline_spread": cpu_spread,
             "host": platform.node(),
         }
         print(json.dumps(line), flush=True)
