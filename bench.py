@@ -3,13 +3,22 @@
 Workload (BASELINE.json north_star headline): synthetic uniform bipartite graph,
 1M users x 1M items, 100M interactions (200M directed nnz of A_hat), dim 64, 3 LightGCN
 layers. A "step" = one full 3-layer forward over the whole graph (gcn_norm cached, as the
-graph is fixed), with the layer mean fused. N GPUs: the rows are sharded over the ranks
-and the propagated embeddings are all-gathered over RCCL after every layer (strong
-scaling: the graph is fixed, value = all nnz x layers / max-over-ranks time).
+graph is fixed), with the layer mean fused. N GPUs (--layout bipartite, the default): users
+and items are sharded separately, each layer propagates one half then the other, and the
+RCCL all-gather of one half's new rows runs on a high-priority stream behind the other
+half's SpMM (strong scaling: the graph is fixed, value = all nnz x layers / max-over-ranks
+time). "roofline" prices the SpMM kernel's algorithmic bytes against HBM peak with its own
+HIP-event time on the stream it runs on.
 
-After the timed steps, a second phase times the masked full-catalog top-20 (e0 scores,
--1024 exclusion of each user's train+val items) for a block of users per rank over all 1M
-items: reported as "topk" (recs/s, aggregated over ranks).
+Phases after the timed steps (each reported in its own key of the same JSON line):
+  topk    masked full-catalog top-20 (e0 scores, -1024 exclusion of each user's train+val
+          items) for a block of users per rank over all 1M items (recs/s over ranks);
+  spread  SpreadLightGCN / LGCNHS for ALL users over all items: item-tiled factored HybridS
+          spreading (no I x I matrix), G (.) F filtered top-20, item ranges sharded over
+          ranks, per-range lists exchanged all-to-all and merged; then "eval": P/R/NDCG/H/I
+          of those lists against a synthetic test split;
+  cpu_baseline*  the reference's op sequences (oracle restatement) on host cores, bounded
+          samples (skip with --no-cpu-baseline).
 
 Run: python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
 """
