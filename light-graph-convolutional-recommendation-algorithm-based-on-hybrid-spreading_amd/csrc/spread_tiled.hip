@@ -515,16 +515,19 @@ __device__ __forceinline__ void load_frag(const float *__restrict__ p, float (&v
 // Merge the tile's columns of (G *) F into running per-user top-K lists (io_val/io_idx,
 // sorted, index -1 = empty). D = 0: no G factor. One wave = NG groups of 16 users (rows);
 // lane (ul, gq) holds user ul of each group and items 4gq..4gq+3 of each 16-item step.
-template <int D, int NG, int M, bool VEC>
+// S = the per-user list stride in LDS (entries): 40 for k <= 24 after a walk's first span
+// (30 KiB blocks: 8 waves per CU, VGPR-limited), else 64*M. (A 3-slot load ring under a
+// 3-waves-per-SIMD register budget spilled and ran 40 % slower.)
+template <int D, int NG, int M, bool VEC, int S>
 __global__ __launch_bounds__(128) void k_tile_topk(
     const double *__restrict__ F, int64_t ldf, int64_t n_rows, int32_t item_begin,
     int32_t n_cols, const float *__restrict__ eu, const float *__restrict__ ei,
     const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col, int drop,
     int k, int first, double *__restrict__ io_val, int64_t *__restrict__ io_idx) {
-  constexpr int CAP = 64 * M;
+  static_assert(S >= 32 && S <= 64 * M, "list stride");
   constexpr int Q = D > 0 ? D / 4 : 1;
-  __shared__ double cs[2][NG][16][CAP];
-  __shared__ int ci[2][NG][16][CAP];
+  __shared__ double cs[2][NG][16][S];
+  __shared__ int ci[2][NG][16][S];
   __shared__ int exs[2][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);  // uniform: SGPR bases
   const int lane = lane_id();
@@ -535,6 +538,7 @@ __global__ __launch_bounds__(128) void k_tile_topk(
   float uf[NG][Q];
   bool uvalid[NG];
   int cnt[NG], chk[NG];
+  bool dirty[NG];  // the user's list gained an entry in this call (first call: always)
   double thr[NG];
   int64_t ex_pos[NG], ex_hi[NG];
   const int lim_end = item_begin + n_cols;
@@ -552,6 +556,7 @@ __global__ __launch_bounds__(128) void k_tile_topk(
     }
     cnt[g] = 0;
     chk[g] = 0;
+    dirty[g] = first != 0;
     thr[g] = uvalid[g] ? neg_inf<double>() : __builtin_huge_val();
   }
   // exclusion cursors: first excluded item >= item_begin, all groups' searches in lockstep
@@ -750,18 +755,19 @@ __global__ __launch_bounds__(128) void k_tile_topk(
               ci[wave][g][ul][p] = item_begin + c0 + r;
             }
             cnt[g] += __popcll(bal & same_user);
+            dirty[g] |= (bal & same_user) != 0;
           }
         }
       }
     }
     bool over = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > S - 16;
     if (__ballot(over)) {
       const int lim = item_begin + (it + 16 < n_cols ? it + 16 : n_cols);
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+        uint64_t need = __ballot(cnt[g] > S - 16) & 0xffffull;
         if (need) {
           wave_sync();
           while (need) {
@@ -803,6 +809,7 @@ __global__ __launch_bounds__(128) void k_tile_topk(
     for (int u = 0; u < 16; ++u) {
       const int64_t r = ubase + g * 16 + u;
       if (r >= n_rows) break;
+      if (!__shfl((int)dirty[g], u)) continue;  // list as loaded: nothing to compact or store
       compact_user(g, u, lim_end);
       const int nc = __shfl(cnt[g], u);
       for (int e = lane; e < k; e += 64) {
@@ -969,31 +976,37 @@ static void launch_tile_topk_v(int M, const double *F, int64_t ldf, int64_t n_ro
                                const int64_t *ex_rowptr, const int32_t *ex_col, int drop,
                                int k, int first, double *io_val, int64_t *io_idx,
                                hipStream_t s) {
-  // LDS per block (2 waves): 2 * NG * 16 * CAP * 12 B = 48 KiB (M=1, NG=2), 48 KiB (M=2,
-  // NG=1), 96 KiB (M=4, NG=1)
-  // LGCNHS_TILE_TOPK_NG1 (A/B knob): one 16-user group per wave at k <= 32 (24 KiB blocks,
-  // twice the waves per CU, one MFMA chain per wave)
-  static int ng1 = -1;
-  if (ng1 < 0) {
-    const char *e = getenv("LGCNHS_TILE_TOPK_NG1");
-    ng1 = e ? atoi(e) : 0;
+  // LDS per block (2 waves): 2 * NG * 16 * S * 12 B (+ 512 B) = 48 KiB (M=1, NG=2, S=64;
+  // 3 blocks = 6 waves per CU), 30 KiB at S=40 (k <= 24: 8 waves per CU, VGPR-limited; the
+  // list is compacted once it holds more than S-16 entries, so the first span of a walk,
+  // where most columns enter, keeps S=64), 48 KiB (M=2), 96 KiB (M=4). Measured per 4096-
+  // column span at 1M users: S=40 8.4-8.6 ms vs S=64 8.8-9.1 ms after the first spans,
+  // 26.4 vs 16.7 ms on the first. LGCNHS_TILE_TOPK_S64=1 (A/B knob) keeps S=64 throughout.
+  static int s64 = -1;
+  if (s64 < 0) {
+    const char *e = getenv("LGCNHS_TILE_TOPK_S64");
+    s64 = e ? atoi(e) : 0;
   }
-  if (M == 1 && ng1) {
-    const unsigned b = (unsigned)((n_rows + 31) / 32);
-    k_tile_topk<D, 1, 1, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
+  if (M == 1 && k <= 24 && !first && !s64) {
+    const unsigned b = (unsigned)((n_rows + 63) / 64);
+    k_tile_topk<D, 2, 1, VEC, 40><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei,
+                                                    ex_rowptr, ex_col, drop, k, first, io_val,
+                                                    io_idx);
   } else if (M == 1) {
     const unsigned b = (unsigned)((n_rows + 63) / 64);
-    k_tile_topk<D, 2, 1, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
+    k_tile_topk<D, 2, 1, VEC, 64><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei,
+                                                    ex_rowptr, ex_col, drop, k, first, io_val,
+                                                    io_idx);
   } else if (M == 2) {
     const unsigned b = (unsigned)((n_rows + 31) / 32);
-    k_tile_topk<D, 1, 2, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
+    k_tile_topk<D, 1, 2, VEC, 128><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei,
+                                                     ex_rowptr, ex_col, drop, k, first, io_val,
+                                                     io_idx);
   } else {
     const unsigned b = (unsigned)((n_rows + 31) / 32);
-    k_tile_topk<D, 1, 4, VEC><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr,
-                                            ex_col, drop, k, first, io_val, io_idx);
+    k_tile_topk<D, 1, 4, VEC, 256><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei,
+                                                     ex_rowptr, ex_col, drop, k, first, io_val,
+                                                     io_idx);
   }
 }
 
