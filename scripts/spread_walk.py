@@ -1,0 +1,34 @@
+"""Time ops.spread_topk_tiled (the pipelined tile walk) over the first --tiles item tiles
+for all users of the C5 graph; with rocprofv3 --kernel-trace the timeline shows whether the
+next tile's W build overlaps the current tile's resource pass (scripts/overlap.py)."""
+import argparse
+import os
+import sys
+import time
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [R, os.path.join(R, "light-graph-convolutional-recommendation-algorithm-based-on-hybrid-spreading_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from lgcnhs import ops  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--tiles", type=int, default=16)
+ap.add_argument("--tile", type=int, default=2048)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+U, I, E, D, _ = bench.WORKLOADS["c5-d64"]
+_, _, keys = bench.gen_graph(U, I, E, 0, dev)
+A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
+del keys
+g = torch.Generator(device=dev).manual_seed(42)
+eu = torch.randn(U, D, device=dev, generator=g) * 0.1
+ei = torch.randn(I, D, device=dev, generator=g) * 0.1
+for rep in range(2):
+    torch.cuda.synchronize()
+    t = time.time()
+    ops.spread_topk_tiled(A, 0.5, 20, A.by_user, eu=eu, ei=ei, tile=a.tile,
+                          items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30)
+    torch.cuda.synchronize()
+    print(f"rep {rep}: {a.tiles} tiles x {U} users: {time.time() - t:.3f} s", flush=True)
