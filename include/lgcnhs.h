@@ -232,7 +232,10 @@ int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
  *             / (alpha[i] * beta[j])          (den == 0 -> 1)
  * written in ascending j as 12-byte entries {int32 j; fp64 value, 4-byte aligned} at
  * wt_ent[wt_ptr[i] .. wt_ptr[i] + len_i), where wt_ptr[n_items + 1] is the exclusive prefix
- * of lg_spread_tile_bound's bounds (row capacities), and wt_meta[i] = wt_ptr[i] |
+ * of the row capacities: lg_spread_tile_bound's bounds, or the bounds rounded up to a
+ * multiple m of entries with 256 % m == 0 (rows then start m*12 bytes apart: m = 32 puts
+ * every row on a 128-B line; a capacity above 256 still means exactly a bound above 256,
+ * the block-per-row path), and wt_meta[i] = wt_ptr[i] |
  * (len_i << 48) (one 8-byte lookup per row for the resource pass); cur/count from
  * lg_spread_tile_cursor, inv_deg from lg_inv_degree_f64 over the user rows. ws:
  * lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in [1, 8192]; every item

@@ -14,6 +14,8 @@ spread_recommend   dense or tiled, whichever fits  model/SpreadMethod/recommend.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -339,6 +341,13 @@ class TileWeights:
         self.j0 = None
         self.width = 0
         self._seek_at = None
+        # Row alignment in entries: 32 x 12 B = 384 B = 3 lines, so a row of n entries spans
+        # ceil(12n / 128) lines instead of one more on average at a random start (the
+        # resource pass gathers ~10^12 entries at C5 and is fabric-bound). Capacities stay
+        # > 256 exactly for the hub rows since 256 is a multiple of 32.
+        self.align = int(os.environ.get("LGCNHS_W_ALIGN", "32"))
+        if self.align < 1 or self.align & (self.align - 1) or 256 % self.align:
+            raise ValueError(f"LGCNHS_W_ALIGN={self.align}: a power of two dividing 256")
 
     @property
     def len(self) -> torch.Tensor:
@@ -391,7 +400,11 @@ class TileWeights:
         N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
                                        N.ptr(self.count), N.ptr(self.bound), strm),
                 "lg_spread_tile_bound")
-        torch.cumsum(self.bound, 0, out=self.ptr[1:])
+        if self.align > 1:  # row capacities rounded up: every row starts on a 128-B line
+            torch.cumsum(torch.bitwise_and(self.bound + (self.align - 1), -self.align), 0,
+                         out=self.ptr[1:])
+        else:
+            torch.cumsum(self.bound, 0, out=self.ptr[1:])
         total = int(self.ptr[-1])  # host sync: sizes the row storage
         if 3 * total > self.ent.numel():
             cap = max(total, int(self.ent.numel() // 3 * 1.25))
