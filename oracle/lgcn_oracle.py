@@ -122,6 +122,30 @@ def lightgcn_forward(edge_index: torch.Tensor, emb_u: torch.Tensor, emb_i: torch
 
 
 # ----------------------------------------------------------------------------------
+# training step: model/LightGCN/train.py:26-59,148-151, model/LightGCN/loss.py:12-43
+# ----------------------------------------------------------------------------------
+def bpr_loss(uf, u0, pf, p0, nf, n0, lambda_val: float):
+    """loss.py:28-43, with its sign: -mean(softplus(pos - neg)) + lambda * sum of squared
+    L2 norms of the batch's e0 rows."""
+    reg = lambda_val * (u0.norm(2).pow(2) + p0.norm(2).pow(2) + n0.norm(2).pow(2))
+    pos = torch.sum(uf * pf, dim=-1)
+    neg = torch.sum(uf * nf, dim=-1)
+    return -torch.mean(torch.nn.functional.softplus(pos - neg)) + reg
+
+
+def bpr_step(edge_index, emb_u, emb_i, layers: int, users, pos, neg, lambda_val: float):
+    """One getEmbeddingForBPR + BPRLoss + backward on leaf copies of (emb_u, emb_i) for
+    fixed (users, pos, neg) triples (train.py:50-57 gathers; item ids are 0-based):
+    returns (loss, grad_u, grad_i)."""
+    eu = emb_u.detach().clone().requires_grad_(True)
+    ei = emb_i.detach().clone().requires_grad_(True)
+    uf, itf = lightgcn_forward(edge_index, eu, ei, layers)
+    loss = bpr_loss(uf[users], eu[users], itf[pos], ei[pos], itf[neg], ei[neg], lambda_val)
+    loss.backward()
+    return loss.detach(), eu.grad, ei.grad
+
+
+# ----------------------------------------------------------------------------------
 # e0 scoring + masks + topk: model/LightGCN/recommend.py:83-114
 # ----------------------------------------------------------------------------------
 def masked_scores_torch(eu: torch.Tensor, ei: torch.Tensor, train_pairs, val_pairs):
