@@ -490,6 +490,7 @@ def main():
     # algorithmic bytes per SpMM launch: nnz*(8+4d) + rows*(4+4d)
     alg_bytes = shard.nnz * (8 + 4 * D) + shard.n_rows * (4 + 4 * D)
     achieved = alg_bytes / avg_kernel_s / 1e9
+    job_bytes = nnz * (8 + 4 * D) + N * (4 + 4 * D)  # one layer of the whole graph
     traffic = load_traffic(args.workload, world)
 
     # the same graph at the other embedding widths the configs name (C5: d=128)
@@ -574,7 +575,12 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel": "lg_spmm_layer_f32",
                          "avg_launch_ms": avg_kernel_s * 1e3,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         # north_star's end-to-end figure: value (all ranks, all-gathers
+                         # included) against N GPUs' HBM-roofline edge-layers/s for the
+                         # whole graph's algorithmic bytes per edge-layer
+                         "job_edge_layers_roofline": world * HBM_PEAK_GBS * 1e9 * nnz / job_bytes,
+                         "job_frac": value / (world * HBM_PEAK_GBS * 1e9 * nnz / job_bytes)},
             "comm": comm,
             "topk": topk,
             "spread": spread,
