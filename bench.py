@@ -266,6 +266,47 @@ def bench_small_config(dev, k):
     return res
 
 
+def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024):
+    """SURVEY.md §8 f2 on the north_star graph, one GPU: the reference's training step
+    (model/LightGCN/train.py:26-59,148-151; loss.py:12-70) through the package's own path:
+    HIP forward (ops.propagate), structured negative sampling of EVERY interaction + a
+    1024-pair mini-batch (model.LightGCN.loss.sampleMiniBatch), BPRLoss, backward (the
+    HIP propagation with A_hat^T = A_hat) and one Adam step over all U+I embedding rows.
+    The interactions here are the train|val positives the other phases exclude."""
+    from lgcnhs import ops
+    from lgcnhs.graph import Adjacency
+    from model.LightGCN.loss import BPRLoss, sampleMiniBatch
+    adj = Adjacency(rowptr, src, U + I, n_users=U, symmetric=True)
+    e0 = torch.nn.Parameter(e0_orig.clone())
+    opt = torch.optim.Adam([e0], lr=1e-3)
+    r_edge = torch.stack([keys // I, keys % I])
+    gen = torch.Generator(device=dev).manual_seed(42)
+
+    def step():
+        out = ops.propagate(adj, e0, L)
+        u, p, n = sampleMiniBatch(batch, r_edge, I, generator=gen)
+        loss = BPRLoss(out[u], e0[u], out[U + p], e0[U + p], out[U + n], e0[U + n], 1e-6)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    res = {"ms_per_step": dt * 1e3, "steps_per_s": 1.0 / dt, "batch": batch,
+           "interactions_sampled": int(keys.numel()), "loss": float(loss.item()),
+           "what": "HIP forward + negative sampling of all interactions + BPR + HIP backward "
+                   "+ Adam over all embedding rows"}
+    del opt, e0, r_edge, adj
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev, n_test=10_000_000):
     """Full top-k evaluation of the C5 recommendations (metrics/accurate.py +
     metrics/diversity.py on the device, lgcnhs.metrics): P / R / NDCG against a synthetic
@@ -412,6 +453,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-topk", action="store_true")
     ap.add_argument("--no-spread", action="store_true")
+    ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
@@ -476,6 +518,13 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(42)
     e0_orig = torch.randn(N, D, device=dev, generator=gen) * 0.1
     cpu_rp, cpu_src = (rowptr, src) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else (None, None)
+    train = None
+    if world == 1 and not args.no_train:
+        try:
+            train = bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev)
+        except Exception as ex:  # a side measurement never hides the main result
+            log(f"train bench failed: {ex!r}")
+        torch.cuda.empty_cache()
     del rowptr
     if cpu_src is None:
         del src
@@ -584,6 +633,7 @@ def main():
             "comm": comm,
             "topk": topk,
             "spread": spread,
+            "train": train,
             "other_dims": extra,
             "c2_ml1m_shape": small,
             "cpu_baseline": cpu,

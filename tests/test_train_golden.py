@@ -65,3 +65,24 @@ def test_gpu_train_steps_match_reference(golden, monkeypatch):
         assert abs(loss.item() - float(g[f"loss_{s + 1}"])) <= LOSS_TOL
         assert np.abs(m.users_emb.weight.detach().cpu().numpy() - g[f"emb_u_{s + 1}"]).max() <= EMB_TOL
         assert np.abs(m.items_emb.weight.detach().cpu().numpy() - g[f"emb_i_{s + 1}"]).max() <= EMB_TOL
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_structured_negative_sampling_properties(seed):
+    """The sampler (reference loss.py:46-70 via PyG structured_negative_sampling): users and
+    positives are the edge list itself, every negative lies in the item range and is never
+    one of that user's positives; sampleMiniBatch draws rows of that triple set. Its RNG
+    stream differs from PyG's, so the properties are checked, not values (unpinned)."""
+    from model.LightGCN.loss import sampleMiniBatch, structured_negative_sampling
+    g = torch.Generator().manual_seed(seed)
+    U, I = 50, 12                      # dense rows: rejection must loop several times
+    keys = torch.unique(torch.randint(0, U * I, (400,), generator=g))
+    ei = torch.stack([keys // I, keys % I])
+    u, p, n = structured_negative_sampling(ei, I, generator=g)
+    assert torch.equal(u, ei[0]) and torch.equal(p, ei[1])
+    assert int(n.min()) >= 0 and int(n.max()) < I
+    assert not bool(torch.isin(u * I + n, keys).any())
+    bu, bp, bn = sampleMiniBatch(64, ei, I, generator=g)
+    assert bu.shape == bp.shape == bn.shape == (64,)
+    assert bool(torch.isin(bu * I + bp, keys).all())
+    assert not bool(torch.isin(bu * I + bn, keys).any())
