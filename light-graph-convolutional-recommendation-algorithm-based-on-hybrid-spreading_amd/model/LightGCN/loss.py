@@ -19,7 +19,9 @@ def structured_negative_sampling(edge_index: torch.Tensor, num_items: int, gener
     (PyG structured_negative_sampling semantics, rejection on the device; negatives are
     drawn from the item range)."""
     u, p = edge_index[0].long(), edge_index[1].long()
-    keys = torch.sort(u * num_items + p).values
+    keys = u * num_items + p
+    if keys.numel() > 1 and not bool((keys[1:] >= keys[:-1]).all()):
+        keys = torch.sort(keys).values   # edge lists from the CSR builders come sorted
     neg = torch.randint(0, num_items, u.shape, device=u.device, generator=generator)
     for _ in range(64):
         q = u * num_items + neg
