@@ -17,8 +17,8 @@ Phases after the timed steps (each reported in its own key of the same JSON line
           spreading (no I x I matrix), G (.) F filtered top-20, item ranges sharded over
           ranks, per-range lists exchanged all-to-all and merged; then "eval": P/R/NDCG/H/I
           of those lists against a synthetic test split;
-  train   (N=1) one LightGCN BPR training step on the same graph: HIP forward, structured
-          negative sampling of every interaction, BPR, HIP backward, Adam;
+  train   (N=1) one LightGCN BPR training step on the same graph: HIP forward, a mini-batch
+          with structured negatives, BPR, HIP backward, Adam;
   cpu_baseline*  the reference's op sequences (oracle restatement) on host cores, bounded
           samples (skip with --no-cpu-baseline).
 
@@ -271,8 +271,8 @@ def bench_small_config(dev, k):
 def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024):
     """SURVEY.md §8 f2 on the north_star graph, one GPU: the reference's training step
     (model/LightGCN/train.py:26-59,148-151; loss.py:12-70) through the package's own path:
-    HIP forward (ops.propagate), structured negative sampling of EVERY interaction + a
-    1024-pair mini-batch (model.LightGCN.loss.sampleMiniBatch), BPRLoss, backward (the
+    HIP forward (ops.propagate), a 1024-triple mini-batch of the interactions with
+    structured negatives (model.LightGCN.loss.sampleMiniBatch), BPRLoss, backward (the
     HIP propagation with A_hat^T = A_hat) and one Adam step over all U+I embedding rows.
     The interactions here are the train|val positives the other phases exclude."""
     from lgcnhs import ops
@@ -302,8 +302,8 @@ def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024
     dt = (time.perf_counter() - t0) / steps
     res = {"ms_per_step": dt * 1e3, "steps_per_s": 1.0 / dt, "batch": batch,
            "interactions_sampled": int(keys.numel()), "loss": float(loss.item()),
-           "what": "HIP forward + negative sampling of all interactions + BPR + HIP backward "
-                   "+ Adam over all embedding rows"}
+           "what": "HIP forward + mini-batch with structured negatives over all interactions + "
+                   "BPR + HIP backward + Adam over all embedding rows"}
     del opt, e0, r_edge, adj
     torch.cuda.empty_cache()
     return res
