@@ -104,6 +104,17 @@ int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src, const float *di
                       int32_t acc_mode, float denom, int64_t long_threshold,
                       lg_stream_t stream);
 
+/* lg_spmm_layer_f32 for a sparse input x (the backward pass of the same call sites,
+ * reference model/LightGCN/train.py:150 `loss.backward()` through model.py:62): live[n]
+ * (uint8, one per source node) == 0 promises that row n of x is all zero, and its gather is
+ * skipped (its contribution is added as 0). Same sums as lg_spmm_layer_f32 when the
+ * promise holds. Long rows (above long_threshold) are left to lg_spmm_long_rows_f32. */
+int lg_spmm_layer_live_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
+                           const float *w, const float *x, float *y, const float *x0,
+                           float *acc, float *out, int64_t n_rows, int64_t row_offset,
+                           int32_t dim, int32_t acc_mode, float denom, int64_t long_threshold,
+                           const uint8_t *live, lg_stream_t stream);
+
 /* The long rows skipped above, cut into segments [seg_beg[s], seg_end[s]) of src/w
  * (seg_node[s] = node id of the segment's row): one wave per segment writes a partial sum
  * into partial[n_seg, dim] (caller-owned workspace), then long row j (node long_node[j],

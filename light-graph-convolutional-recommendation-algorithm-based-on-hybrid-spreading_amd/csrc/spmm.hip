@@ -28,6 +28,12 @@
 // cuts them into segments, k_spmm_segments gives each segment its own wave (partial sums
 // in a workspace) and k_spmm_long_reduce adds a row's segments in order and runs the same
 // epilogue. Still atomic-free and bitwise reproducible.
+//
+// Sparse inputs (the backward pass: dL/d(e_final) is non-zero only on the mini-batch's
+// rows, and one layer later only on their neighbours): lg_spmm_layer_live_f32 takes a
+// per-source-node byte mask and skips the 4*D-byte gather of rows marked dead (their
+// contribution w*0 = 0 is added as a register zero, so the sums are the unmasked kernel's).
+// The edge ids and weights are still streamed: 8 B/edge instead of 8 + 4*D.
 #include "common.h"
 
 namespace lg {
@@ -48,12 +54,13 @@ __device__ __forceinline__ void add4(float4 &a, const float4 &b) {
 
 // sum over entries [beg, end) of w_e * x[src_e] for this lane's float4 slice, combined over
 // the wave's lane groups (every group ends with the full sum).
-template <int D, int UNROLL>
+template <int D, int UNROLL, bool LIVE = false>
 __device__ __forceinline__ float4 gather_sum(int64_t beg, int64_t end,
                                              const int32_t *__restrict__ src,
                                              const float *__restrict__ w,
                                              const float *__restrict__ dis, float dg,
-                                             const float *__restrict__ x) {
+                                             const float *__restrict__ x,
+                                             const uint8_t *__restrict__ live = nullptr) {
   constexpr int LPR = D / 4;
   constexpr int G = 64 / LPR;
   const int lane = lane_id();
@@ -65,25 +72,34 @@ __device__ __forceinline__ float4 gather_sum(int64_t beg, int64_t end,
     const int n = (int)((end - cb) < 64 ? (end - cb) : 64);
     int my_s = 0;
     float my_w = 0.f;
+    int my_l = 0;  // LIVE: this lane's edge source row is non-zero (one load per 64 edges)
     if (lane < n) {
       my_s = __builtin_nontemporal_load(src + cb + lane);
       // PyG: deg_inv_sqrt[row] * edge_weight(=1) * deg_inv_sqrt[col]; row = source.
       my_w = w ? __builtin_nontemporal_load(w + cb + lane) : __fmul_rn(dis[my_s], dg);
+      if constexpr (LIVE) my_l = live[my_s];
     }
     for (int j0 = 0; j0 < n; j0 += UNROLL * G) {
       int s[UNROLL];
       float wv[UNROLL];
       float4 xv[UNROLL];
+      int lv[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const int jj = j0 + u * G + gi;
         s[u] = __shfl(my_s, jj & 63);
         wv[u] = __shfl(my_w, jj & 63);
+        if constexpr (LIVE) lv[u] = __shfl(my_l, jj & 63);
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const int jj = j0 + u * G + gi;
-        if (jj < n) xv[u] = x4[(int64_t)s[u] * LPR + li];
+        if constexpr (LIVE) {
+          xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (lv[u]) xv[u] = x4[(int64_t)s[u] * LPR + li];  // 0 for lanes >= n
+        } else {
+          if (jj < n) xv[u] = x4[(int64_t)s[u] * LPR + li];
+        }
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
@@ -136,12 +152,13 @@ __device__ __forceinline__ void epilogue(int64_t g, int li, const float4 &sum,
   }
 }
 
-template <int D, int UNROLL>
+template <int D, int UNROLL, bool LIVE>
 __global__ __launch_bounds__(256) void k_spmm_layer(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ src,
     const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
     float *__restrict__ y, const float *__restrict__ x0, float *acc, float *out,
-    int64_t n_rows, int64_t row_offset, int mode, float denom, int64_t long_threshold) {
+    int64_t n_rows, int64_t row_offset, int mode, float denom, int64_t long_threshold,
+    const uint8_t *__restrict__ live) {
   constexpr int LPR = D / 4;
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (r >= n_rows) return;  // wave-uniform
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(256) void k_spmm_layer(
   const int64_t end = rowptr[r + 1];
   if (end - beg > long_threshold) return;  // done by the segmented path
   const int64_t g = row_offset + r;
-  const float4 sum = gather_sum<D, UNROLL>(beg, end, src, w, dis, dis[g], x);
+  const float4 sum = gather_sum<D, UNROLL, LIVE>(beg, end, src, w, dis, dis[g], x, live);
   const int lane = lane_id();
   if (lane / LPR != 0) return;
   epilogue<D>(g, lane % LPR, sum, y, x0, acc, out, mode, denom);
@@ -194,13 +211,18 @@ template <int D>
 static void launch_spmm(const int64_t *rowptr, const int32_t *src, const float *dis,
                         const float *w, const float *x, float *y, const float *x0, float *acc,
                         float *out, int64_t n_rows, int64_t row_offset, int mode, float denom,
-                        int64_t long_threshold, hipStream_t stream) {
+                        int64_t long_threshold, const uint8_t *live, hipStream_t stream) {
   constexpr int WPB = 4;  // waves (rows) per 256-thread block
   constexpr int UNROLL = (D <= 64) ? 4 : 8;
   const int64_t blocks = (n_rows + WPB - 1) / WPB;
-  k_spmm_layer<D, UNROLL><<<dim3((unsigned)blocks), dim3(64 * WPB), 0, stream>>>(
-      rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
-      long_threshold);
+  if (live)
+    k_spmm_layer<D, UNROLL, true><<<dim3((unsigned)blocks), dim3(64 * WPB), 0, stream>>>(
+        rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
+        long_threshold, live);
+  else
+    k_spmm_layer<D, UNROLL, false><<<dim3((unsigned)blocks), dim3(64 * WPB), 0, stream>>>(
+        rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
+        long_threshold, nullptr);
 }
 
 template <int D>
@@ -237,27 +259,47 @@ static int check_modes(int acc_mode, const float *x0, const float *acc, const fl
 
 using namespace lg;
 
-extern "C" int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src,
-                                 const float *dis, const float *w, const float *x, float *y,
-                                 const float *x0, float *acc, float *out, int64_t n_rows,
-                                 int64_t row_offset, int32_t dim, int32_t acc_mode,
-                                 float denom, int64_t long_threshold, lg_stream_t stream) {
+static int spmm_layer(const int64_t *rowptr, const int32_t *src, const float *dis,
+                      const float *w, const float *x, float *y, const float *x0, float *acc,
+                      float *out, int64_t n_rows, int64_t row_offset, int32_t dim,
+                      int32_t acc_mode, float denom, int64_t long_threshold,
+                      const uint8_t *live, lg_stream_t stream, const char *fn) {
   LG_REQUIRE(rowptr && dis && x && n_rows >= 0 && row_offset >= 0,
-             "lg_spmm_layer_f32: null pointer or negative size");
+             "%s: null pointer or negative size", fn);
   LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
-             "lg_spmm_layer_f32: dim %d not in {32,64,128,256}", dim);
-  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, "lg_spmm_layer_f32");
+             "%s: dim %d not in {32,64,128,256}", fn, dim);
+  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, fn);
   if (st != LG_OK) return st;
   if (n_rows == 0) return LG_OK;
   if (long_threshold <= 0) long_threshold = INT64_MAX;
   hipStream_t s = (hipStream_t)stream;
   switch (dim) {
-    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
-    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
-    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
-    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, s); break;
+    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
+    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
+    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
+    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
   }
-  return launch_status("lg_spmm_layer_f32");
+  return launch_status(fn);
+}
+
+extern "C" int lg_spmm_layer_f32(const int64_t *rowptr, const int32_t *src,
+                                 const float *dis, const float *w, const float *x, float *y,
+                                 const float *x0, float *acc, float *out, int64_t n_rows,
+                                 int64_t row_offset, int32_t dim, int32_t acc_mode,
+                                 float denom, int64_t long_threshold, lg_stream_t stream) {
+  return spmm_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, dim,
+                    acc_mode, denom, long_threshold, nullptr, stream, "lg_spmm_layer_f32");
+}
+
+extern "C" int lg_spmm_layer_live_f32(const int64_t *rowptr, const int32_t *src,
+                                      const float *dis, const float *w, const float *x,
+                                      float *y, const float *x0, float *acc, float *out,
+                                      int64_t n_rows, int64_t row_offset, int32_t dim,
+                                      int32_t acc_mode, float denom, int64_t long_threshold,
+                                      const uint8_t *live, lg_stream_t stream) {
+  LG_REQUIRE(live, "lg_spmm_layer_live_f32: null live mask");
+  return spmm_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, dim,
+                    acc_mode, denom, long_threshold, live, stream, "lg_spmm_layer_live_f32");
 }
 
 extern "C" int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_end,

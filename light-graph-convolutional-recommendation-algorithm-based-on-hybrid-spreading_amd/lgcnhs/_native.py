@@ -42,6 +42,11 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _f32, _i64, _vp],
     ),
+    "lg_spmm_layer_live_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _f32, _i64, _vp,
+         _vp],
+    ),
     "lg_spmm_long_rows_f32": (
         ctypes.c_int,
         [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,

@@ -33,16 +33,25 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------ propagation
 def run_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows: int, row_offset: int,
-              mode: int, denom: float, plan=None) -> None:
-    """One propagation layer over a CSR slice: lg_spmm_layer_f32 for the ordinary rows and,
-    when the slice has rows above the long-row threshold, lg_spmm_long_rows_f32 for them."""
+              mode: int, denom: float, plan=None, live=None) -> None:
+    """One propagation layer over a CSR slice: lg_spmm_layer_f32 for the ordinary rows (or
+    lg_spmm_layer_live_f32 when a uint8 per-node ``live`` mask marks x's non-zero rows)
+    and, when the slice has rows above the long-row threshold, lg_spmm_long_rows_f32."""
     dim = x.shape[1]
     thr = plan.threshold if (plan is not None and plan.n_long) else 0
     strm = N.stream_handle(x.device)
-    N.check(N.lib().lg_spmm_layer_f32(
-        N.ptr(rowptr), N.ptr(src), N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0),
-        N.ptr(acc), N.ptr(out), n_rows, row_offset, dim, mode, float(denom), thr, strm),
-        "lg_spmm_layer_f32")
+    if live is not None:
+        if live.dtype != torch.uint8 or live.numel() != x.shape[0] or live.device != x.device:
+            raise ValueError("live must be a uint8 mask with one entry per row of x")
+        N.check(N.lib().lg_spmm_layer_live_f32(
+            N.ptr(rowptr), N.ptr(src), N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0),
+            N.ptr(acc), N.ptr(out), n_rows, row_offset, dim, mode, float(denom), thr,
+            N.ptr(live), strm), "lg_spmm_layer_live_f32")
+    else:
+        N.check(N.lib().lg_spmm_layer_f32(
+            N.ptr(rowptr), N.ptr(src), N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0),
+            N.ptr(acc), N.ptr(out), n_rows, row_offset, dim, mode, float(denom), thr, strm),
+            "lg_spmm_layer_f32")
     if thr:
         part = plan.partial(dim, x.device)
         N.check(N.lib().lg_spmm_long_rows_f32(
@@ -53,17 +62,29 @@ def run_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows: int, row_offset: 
 
 
 def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
-               stream_weights: bool = True, long_rows: bool = True) -> None:
+               stream_weights: bool = True, long_rows: bool = True, live=None) -> None:
     """One layer over all rows of ``adj``; with stream_weights the precomputed gcn_norm
     edge weights are streamed (else recomputed from dis; identical values); with
     long_rows, hub rows go through the segmented path."""
     w = adj.edge_weight() if stream_weights else None
     run_layer(adj.rowptr, adj.src, adj.dis(), w, x, y, x0, acc, out, adj.n_nodes, 0, mode,
-              denom, adj.long_plan() if long_rows else None)
+              denom, adj.long_plan() if long_rows else None, live)
 
 
-def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:
-    """mean_{l=0..L} A_hat^l e0 with A_hat = D^-1/2 A D^-1/2 (no autograd)."""
+LIVE_FRACTION = 0.25  # below this share of non-zero input rows, skip the dead rows' gathers
+
+
+def live_rows(x: torch.Tensor) -> torch.Tensor:
+    """uint8 [rows]: 1 where row of x has a non-zero entry."""
+    return (x != 0).any(dim=1).to(torch.uint8)
+
+
+def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int,
+                   sparse_input: bool = False) -> torch.Tensor:
+    """mean_{l=0..L} A_hat^l e0 with A_hat = D^-1/2 A D^-1/2 (no autograd). With
+    sparse_input (the backward pass: e0 = dL/d(e_final), non-zero on a mini-batch's rows),
+    each layer whose input has < LIVE_FRACTION non-zero rows gathers only those rows
+    (lg_spmm_layer_live_f32; same sums)."""
     e0 = _f32(e0, "e0")
     if e0.shape[0] != adj.n_nodes:
         raise ValueError(f"e0 has {e0.shape[0]} rows, graph has {adj.n_nodes} nodes")
@@ -83,7 +104,12 @@ def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tenso
         else:
             mode = N.LG_ACC_MID
         y = None if last else bufs[l % 2]
-        spmm_layer(adj, x, y, e0, out, out, mode, layers + 1)
+        live = None
+        if sparse_input:
+            live = live_rows(x)
+            if int(live.sum()) >= LIVE_FRACTION * live.numel():
+                live, sparse_input = None, False   # dense from here on
+        spmm_layer(adj, x, y, e0, out, out, mode, layers + 1, live=live)
         x = y
     return out
 
@@ -127,7 +153,8 @@ class _Propagate(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        gin = propagate_mean(ctx.adj.transpose(), g.contiguous(), ctx.layers)
+        gin = propagate_mean(ctx.adj.transpose(), g.contiguous(), ctx.layers,
+                             sparse_input=True)
         return gin, None, None
 
 

@@ -229,3 +229,37 @@ def test_sharded_layouts_single_rank_equal_propagate(cls, chunks):
         prop = BipartitePropagation(sh, sh.permute_rows(adj.dis()), d, L, "cuda")
     got = sh.unpermute_rows(prop.forward(sh.permute_rows(e0)))
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+@pytest.mark.parametrize("dim", [64, 128])
+def test_live_mask_backward_equals_dense(dist, dim):
+    """The backward of a mini-batch loss: the input gradient is non-zero on a few rows, so
+    the sparse-input layers (lg_spmm_layer_live_f32) skip the dead rows' gathers. The sums
+    equal the dense kernel's bitwise (zero rows add 0), including hub rows on the segmented
+    path, and the autograd gradient equals the dense propagate of the same gradient."""
+    from lgcnhs import ops, _native as N
+    from lgcnhs.graph import Adjacency
+    U, I, E = (60_000, 5_000, 600_000) if dist == "zipf" else (40_000, 30_000, 800_000)
+    users, items = _synth_graph(U, I, E, seed=5, dist=dist)
+    adj = Adjacency.from_interactions(torch.as_tensor(users), torch.as_tensor(items), U, I, DEV)
+    n = U + I
+    g = torch.zeros(n, dim, device=DEV)
+    rows = torch.randint(0, n, (700,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    g[rows] = torch.randn(rows.numel(), dim, device=DEV)
+    live = ops.live_rows(g)
+    assert int(live.sum()) == int(torch.unique(rows).numel())
+    y1, y2 = torch.empty_like(g), torch.empty_like(g)
+    ops.spmm_layer(adj, g, y1, None, None, None, N.LG_ACC_NONE, 1.0)
+    ops.spmm_layer(adj, g, y2, None, None, None, N.LG_ACC_NONE, 1.0, live=live)
+    assert torch.equal(y1, y2)
+    dense = ops.propagate_mean(adj, g, 3)
+    sparse = ops.propagate_mean(adj, g, 3, sparse_input=True)
+    assert torch.equal(dense, sparse)
+    e0 = (torch.randn(n, dim, device=DEV) * 0.1).requires_grad_(True)
+    out = ops.propagate(adj, e0, 3)
+    (out * g).sum().backward()
+    assert torch.equal(e0.grad, dense)
+    with pytest.raises(ValueError):
+        ops.spmm_layer(adj, g, y2, None, None, None, N.LG_ACC_NONE, 1.0,
+                       live=live.to(torch.int32))

@@ -43,6 +43,10 @@ def test_argument_validation_without_gpu():
     assert st == 1 and b"excl_mode" in lib.lg_last_error()
     st = lib.lg_spmm_layer_f32(one, one, one, z, one, one, z, z, z, 5, 0, 64, 3, 4.0, 0, z)
     assert st == 1  # LAST needs acc/out
+    st = lib.lg_spmm_layer_live_f32(one, one, one, z, one, z, z, z, z, 10, 0, 64, 0, 1.0, 0, z, z)
+    assert st == 1 and b"live" in lib.lg_last_error()
+    st = lib.lg_spmm_layer_live_f32(one, one, one, z, one, z, z, z, z, 10, 0, 48, 0, 1.0, 0, one, z)
+    assert st == 1 and b"lg_spmm_layer_live_f32" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
 
