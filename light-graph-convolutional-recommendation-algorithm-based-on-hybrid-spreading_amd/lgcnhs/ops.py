@@ -107,8 +107,12 @@ def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int,
         live = None
         if sparse_input:
             live = live_rows(x)
-            if int(live.sum()) >= LIVE_FRACTION * live.numel():
-                live, sparse_input = None, False   # dense from here on
+            frac = int(live.sum()) / max(1, live.numel())
+            if frac >= LIVE_FRACTION:
+                live = None
+            # the next input's non-zero rows are this one's neighbours: stop checking once
+            # they are expected to pass the threshold (a mask pass + sync saved per layer)
+            sparse_input = frac * adj.nnz / max(1, adj.n_nodes) < LIVE_FRACTION
         spmm_layer(adj, x, y, e0, out, out, mode, layers + 1, live=live)
         x = y
     return out
