@@ -68,16 +68,38 @@ __device__ __forceinline__ float4 gather_sum(int64_t beg, int64_t end,
   const int li = lane % LPR;
   const float4 *__restrict__ x4 = reinterpret_cast<const float4 *>(x);
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  // LIVE: the next 64 edges' ids/weights are loaded while this chunk's mask bytes are in
+  // flight (the chain edge id -> mask byte bounds the layer, not bandwidth)
+  int nx_s = 0;
+  float nx_w = 0.f;
+  if constexpr (LIVE) {
+    if (beg + lane < end) {
+      nx_s = __builtin_nontemporal_load(src + beg + lane);
+      nx_w = w ? __builtin_nontemporal_load(w + beg + lane) : __fmul_rn(dis[nx_s], dg);
+    }
+  }
   for (int64_t cb = beg; cb < end; cb += 64) {
     const int n = (int)((end - cb) < 64 ? (end - cb) : 64);
     int my_s = 0;
     float my_w = 0.f;
     int my_l = 0;  // LIVE: this lane's edge source row is non-zero (one load per 64 edges)
-    if (lane < n) {
+    if constexpr (LIVE) {
+      my_s = nx_s;
+      my_w = nx_w;
+      if (lane < n) my_l = live[my_s];
+      nx_s = 0;
+      nx_w = 0.f;
+      if (cb + 64 + lane < end) {
+        nx_s = __builtin_nontemporal_load(src + cb + 64 + lane);
+        nx_w = w ? __builtin_nontemporal_load(w + cb + 64 + lane) : __fmul_rn(dis[nx_s], dg);
+      }
+      // no live source in the chunk: its terms are all +0 and sum is never -0, so
+      // skipping them leaves the sum bitwise unchanged
+      if (__ballot(my_l) == 0) continue;
+    } else if (lane < n) {
       my_s = __builtin_nontemporal_load(src + cb + lane);
       // PyG: deg_inv_sqrt[row] * edge_weight(=1) * deg_inv_sqrt[col]; row = source.
       my_w = w ? __builtin_nontemporal_load(w + cb + lane) : __fmul_rn(dis[my_s], dg);
-      if constexpr (LIVE) my_l = live[my_s];
     }
     for (int j0 = 0; j0 < n; j0 += UNROLL * G) {
       int s[UNROLL];
