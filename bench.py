@@ -62,28 +62,8 @@ def log(*a):
 def gen_graph(U, I, E, seed, dev):
     """Exactly E unique uniform (user, item) pairs on the device; returns the symmetric
     CSR over U+I nodes (rowptr int64, src int32) plus the sorted interaction keys."""
-    from lgcnhs.graph import _rowptr_from_sorted
-    g = torch.Generator(device=dev).manual_seed(seed)
-    keys = torch.empty(0, dtype=torch.int64, device=dev)
-    while keys.numel() < E:
-        n = int((E - keys.numel()) * 1.02) + 1024
-        u = torch.randint(0, U, (n,), device=dev, generator=g)
-        i = torch.randint(0, I, (n,), device=dev, generator=g)
-        keys = torch.unique(torch.cat([keys, u * I + i]))
-        del u, i
-    if keys.numel() > E:
-        pick = torch.randperm(keys.numel(), device=dev, generator=g)[:E]
-        keys = torch.sort(keys[pick]).values
-    users = keys // I
-    items = keys % I
-    ikeys = torch.sort(items * U + users).values
-    n = U + I
-    rows = torch.cat([users, (ikeys // U) + U])          # users then items: sorted
-    src = torch.cat([items + U, ikeys % U]).to(torch.int32)
-    del ikeys, items
-    rowptr = _rowptr_from_sorted(rows, n)
-    del rows
-    return rowptr, src, keys
+    from lgcnhs.synth import synth_graph_device
+    return synth_graph_device(U, I, E, seed, dev)
 
 
 def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):

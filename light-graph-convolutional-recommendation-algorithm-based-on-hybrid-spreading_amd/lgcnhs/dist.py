@@ -1,19 +1,22 @@
 """Row-sharded multi-GPU propagation: one process per GPU, RCCL all-gather over xGMI,
 overlapped with the SpMM.
 
-SURVEY.md §8(e). Rank r owns the contiguous original rows [r*C*S, (r+1)*C*S) of A_hat
-(equal row counts; the benchmark's uniform graphs are nnz-balanced that way), cut into C
-sub-chunks of S rows. Every rank keeps a full replica of the layer input x. Per layer it
-runs the SpMM kernel on one sub-chunk at a time and, as soon as sub-chunk c is done,
-starts an asynchronous ``all_gather_into_tensor`` of it (RCCL runs on its own stream)
+SURVEY.md §8(e). The rows of A_hat are cut into W*C contiguous pieces balanced by
+NON-ZEROS (cumulative rowptr search: every piece holds ~nnz/(W*C) edges, so a Zipf graph's
+hub rows do not pile onto one rank); rank r owns pieces r*C .. r*C+C-1, i.e. a contiguous
+run of rows, worked as C sub-chunks. Every rank keeps a full replica of the layer input x.
+Per layer it runs the SpMM kernel on one sub-chunk at a time and, as soon as sub-chunk c is
+done, starts an asynchronous ``all_gather_into_tensor`` of it (RCCL runs on its own stream)
 while the kernel works on sub-chunk c+1; the next layer waits for all C gathers. Only the
 last gather of a layer is exposed.
 
-For the gathers to land in place, node ids live in a *chunk-major* layout:
-    new(g) = c*(W*S) + r*S + i      for original g = r*(C*S) + c*S + i
+For the gathers to land in place, node ids live in a *chunk-major* layout where every piece
+is padded to the longest piece's S rows:
+    new(g) = c*(W*S) + r*S + (g - start(r, c))      for g in piece (r, c)
 so sub-chunk c of every rank is one contiguous block of W*S rows in rank order, which is
 exactly what ``all_gather_into_tensor`` writes. ``src`` ids, dis and e0 are permuted into
-that layout once; the output is permuted back on demand. C = 1 is the plain row shard.
+that layout once; the output is permuted back on demand. C = 1 is the plain row shard;
+``balance="rows"`` restores equal row counts (S = ceil(n / (W*C))).
 
 The per-shard layer is pluggable so the bookkeeping can run on CPU with gloo
 (tests/test_dist_gloo.py); on GPUs it is lg_spmm_layer_f32.
@@ -37,19 +40,67 @@ def acc_mode(l: int, layers: int) -> int:
     return 2  # LG_ACC_MID
 
 
+def piece_bounds(rowptr: torch.Tensor, lo: int, hi: int, parts: int,
+                 balance: str = "nnz") -> list:
+    """parts+1 row boundaries cutting rows [lo, hi) into contiguous pieces: by cumulative
+    non-zeros (piece p ends at the first row whose prefix reaches (p+1)/parts of the
+    range's edges) or, with balance="rows", into pieces of ceil((hi-lo)/parts) rows."""
+    lo, hi = int(lo), int(hi)
+    if balance == "rows":
+        S = -(-(hi - lo) // parts) if hi > lo else 0
+        return [min(hi, lo + p * S) for p in range(parts)] + [hi]
+    if balance != "nnz":
+        raise ValueError(f"balance must be 'nnz' or 'rows', got {balance!r}")
+    rp = rowptr[lo:hi + 1].to(torch.int64).cpu()
+    total = int(rp[-1] - rp[0])
+    if total == 0:
+        return piece_bounds(rowptr, lo, hi, parts, "rows")
+    targets = torch.tensor([int(rp[0]) + (p * total + parts - 1) // parts
+                            for p in range(1, parts)], dtype=torch.int64)
+    cuts = torch.searchsorted(rp, targets).tolist()
+    b = [lo] + [lo + int(c) for c in cuts] + [hi]
+    for p in range(1, len(b)):  # monotone
+        b[p] = max(b[p], b[p - 1])
+    return b
+
+
+class _Layout:
+    """Piece table of a chunk-major layout: piece P covers original rows
+    [start[P], start[P] + len) and lands at layout row offset[P]."""
+
+    def __init__(self, starts: list, offsets: list):
+        self.starts = torch.tensor(starts, dtype=torch.int64)
+        self.offsets = torch.tensor(offsets, dtype=torch.int64)
+
+    def map(self, g: torch.Tensor) -> torch.Tensor:
+        st, off = self.starts.to(g.device), self.offsets.to(g.device)
+        P = torch.searchsorted(st, g, right=True) - 1
+        return off[P] + (g - st[P])
+
+
 class RowShard:
     """This rank's rows of a CSR over n_nodes nodes, in the chunk-major layout."""
 
     def __init__(self, rowptr: torch.Tensor, src: torch.Tensor, n_nodes: int, rank: int,
                  world: int, device=None, weight: torch.Tensor | None = None,
-                 chunks: int = 1):
+                 chunks: int = 1, balance: str = "nnz"):
         self.n_nodes, self.rank, self.world, self.chunks = int(n_nodes), rank, world, chunks
-        self.S = math.ceil(self.n_nodes / (world * chunks))
-        self.n_pad = self.S * world * chunks
+        W, C = world, chunks
+        self.bounds = piece_bounds(rowptr, 0, self.n_nodes, W * C, balance)
+        lens = [self.bounds[p + 1] - self.bounds[p] for p in range(W * C)]
+        self.S = max(1, max(lens))
+        self.n_pad = self.S * W * C
         dev = device if device is not None else rowptr.device
         self.device = dev
-        g0 = min(rank * chunks * self.S, self.n_nodes)
-        g1 = min(self.n_nodes, g0 + chunks * self.S)
+        starts, offsets, piece_off = [], [], []
+        for p in range(W * C):
+            r, c = p // C, p % C
+            piece_off.append(c * W * self.S + r * self.S)
+            if lens[p]:
+                starts.append(self.bounds[p])
+                offsets.append(piece_off[p])
+        self._layout = _Layout(starts or [0], offsets or [0])
+        g0, g1 = self.bounds[rank * C], self.bounds[(rank + 1) * C]
         b, e = int(rowptr[g0]), int(rowptr[g1])
         self.g0, self.g1 = g0, g1
         self.rowptr = (rowptr[g0:g1 + 1] - b).to(dev)
@@ -60,9 +111,8 @@ class RowShard:
         # (local row begin, local row end, output row offset) per sub-chunk
         self.pieces = []
         for c in range(chunks):
-            lb = min(c * self.S, g1 - g0)
-            le = min((c + 1) * self.S, g1 - g0)
-            self.pieces.append((lb, le, c * world * self.S + rank * self.S))
+            p = rank * C + c
+            self.pieces.append((self.bounds[p] - g0, self.bounds[p + 1] - g0, piece_off[p]))
 
     @property
     def n_rows(self) -> int:
@@ -71,10 +121,7 @@ class RowShard:
     # ------------------------------------------------------------------ layout maps
     def to_layout(self, g: torch.Tensor) -> torch.Tensor:
         """original node id -> chunk-major id."""
-        CS = self.chunks * self.S
-        r, o = g // CS, g % CS
-        c, i = o // self.S, o % self.S
-        return c * (self.world * self.S) + r * self.S + i
+        return self._layout.map(g)
 
     def permute_rows(self, t: torch.Tensor) -> torch.Tensor:
         """[n_nodes, ...] in original order -> [n_pad, ...] chunk-major (zero padding)."""
@@ -159,17 +206,18 @@ class ShardedPropagation:
 # ------------------------------------------------------- bipartite-ordered propagation
 class SegmentShard:
     """This rank's rows when the node ids form contiguous segments that are sharded
-    separately: for LightGCN, users [0, U) and items [U, U+I). Rank r owns sub-chunk r of
-    every segment (a share of the users AND a share of the items), each cut into C pieces of
-    S_s rows. Layout: segment-major, then chunk-major inside a segment,
-        new(g) = base_s + c*(W*S_s) + r*S_s + i     for g = start_s + r*(C*S_s) + c*S_s + i,
+    separately: for LightGCN, users [0, U) and items [U, U+I). Each segment is cut into
+    W*C pieces balanced by non-zeros (piece_bounds) and padded to its longest piece's S_s
+    rows; rank r owns pieces r*C .. r*C+C-1 of every segment (a share of the users' edges AND
+    of the items' edges). Layout: segment-major, then chunk-major inside a segment,
+        new(g) = base_s + c*(W*S_s) + r*S_s + (g - start_s(r, c)),
     so piece (s, c) of every rank is one contiguous block that all_gather_into_tensor writes
     in place. Exposes the interface of RowShard (rowptr/src/weight/pieces, to_layout,
     permute_rows) plus ``seg_pieces[s]``."""
 
     def __init__(self, rowptr: torch.Tensor, src: torch.Tensor, bounds: list, rank: int,
                  world: int, device=None, weight: torch.Tensor | None = None,
-                 chunks: int = 1):
+                 chunks: int = 1, balance: str = "nnz"):
         self.bounds = [int(b) for b in bounds]
         self.n_nodes = self.bounds[-1]
         self.rank, self.world, self.chunks = rank, world, chunks
@@ -177,22 +225,29 @@ class SegmentShard:
         self.device = dev
         W, C = world, chunks
         nseg = len(self.bounds) - 1
-        self.S, self.base = [], []
+        self.S, self.base, self.cuts = [], [], []
+        starts, offsets = [], []
         base = 0
         for s in range(nseg):
-            n_s = self.bounds[s + 1] - self.bounds[s]
-            S_s = math.ceil(n_s / (W * C)) if n_s else 0
+            cuts = piece_bounds(rowptr, self.bounds[s], self.bounds[s + 1], W * C, balance)
+            lens = [cuts[p + 1] - cuts[p] for p in range(W * C)]
+            S_s = max(lens) if self.bounds[s + 1] > self.bounds[s] else 0
             self.S.append(S_s)
             self.base.append(base)
+            self.cuts.append(cuts)
+            for p in range(W * C):
+                if lens[p]:
+                    starts.append(cuts[p])
+                    offsets.append(base + (p % C) * W * S_s + (p // C) * S_s)
             base += W * C * S_s
         self.n_pad = base
+        self._layout = _Layout(starts or [0], offsets or [0])
         rp_parts, src_parts, w_parts = [], [], []
         self.seg_pieces, self.ranges = [], []
         lrow, lent = 0, 0
         for s in range(nseg):
-            st, en, S_s = self.bounds[s], self.bounds[s + 1], self.S[s]
-            g0 = min(st + rank * C * S_s, en)
-            g1 = min(en, g0 + C * S_s)
+            cuts, S_s = self.cuts[s], self.S[s]
+            g0, g1 = cuts[rank * C], cuts[(rank + 1) * C]
             self.ranges.append((g0, g1))
             b, e = int(rowptr[g0]), int(rowptr[g1])
             rp_parts.append((rowptr[g0:g1] - b + lent) if g1 > g0 else rowptr[:0])
@@ -201,9 +256,9 @@ class SegmentShard:
                 w_parts.append(weight[b:e])
             pieces = []
             for c in range(C):
-                lb = min(c * S_s, g1 - g0)
-                le = min((c + 1) * S_s, g1 - g0)
-                pieces.append((lrow + lb, lrow + le, self.base[s] + c * W * S_s + rank * S_s))
+                p = rank * C + c
+                pieces.append((lrow + cuts[p] - g0, lrow + cuts[p + 1] - g0,
+                               self.base[s] + c * W * S_s + rank * S_s))
             self.seg_pieces.append(pieces)
             lrow += g1 - g0
             lent += e - b
@@ -222,16 +277,7 @@ class SegmentShard:
 
     def to_layout(self, g: torch.Tensor) -> torch.Tensor:
         """original node id -> layout id."""
-        b = torch.tensor(self.bounds[1:-1], dtype=torch.int64, device=g.device)
-        seg = torch.bucketize(g, b, right=True)
-        st = torch.tensor(self.bounds[:-1], dtype=torch.int64, device=g.device)[seg]
-        S = torch.tensor(self.S, dtype=torch.int64, device=g.device)[seg].clamp_min(1)
-        base = torch.tensor(self.base, dtype=torch.int64, device=g.device)[seg]
-        o = g - st
-        CS = self.chunks * S
-        r, rem = o // CS, o % CS
-        c, i = rem // S, rem % S
-        return base + c * (self.world * S) + r * S + i
+        return self._layout.map(g)
 
     def permute_rows(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.zeros((self.n_pad,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)

@@ -61,6 +61,36 @@ def synth_interactions(n_users: int, n_items: int, n_edges: int, seed: int = 0,
     return keys // I, keys % I
 
 
+def synth_graph_device(n_users: int, n_items: int, n_edges: int, seed: int, device):
+    """Exactly n_edges unique uniform (user, item) pairs drawn on the device (the C4/C5
+    scale, where numpy's unique over 10^8 keys is too slow). Returns the symmetric CSR over
+    U+I nodes (rowptr int64, src int32; users then items, each row ascending) and the sorted
+    interaction keys user * I + item (int64)."""
+    import torch
+
+    from .graph import _rowptr_from_sorted
+    U, I, E = int(n_users), int(n_items), int(n_edges)
+    g = torch.Generator(device=device).manual_seed(seed)
+    keys = torch.empty(0, dtype=torch.int64, device=device)
+    while keys.numel() < E:
+        n = int((E - keys.numel()) * 1.02) + 1024
+        u = torch.randint(0, U, (n,), device=device, generator=g)
+        i = torch.randint(0, I, (n,), device=device, generator=g)
+        keys = torch.unique(torch.cat([keys, u * I + i]))
+        del u, i
+    if keys.numel() > E:
+        pick = torch.randperm(keys.numel(), device=device, generator=g)[:E]
+        keys = torch.sort(keys[pick]).values
+    users = keys // I
+    items = keys % I
+    ikeys = torch.sort(items * U + users).values
+    rows = torch.cat([users, (ikeys // U) + U])          # users then items: sorted
+    src = torch.cat([items + U, ikeys % U]).to(torch.int32)
+    del ikeys, items
+    rowptr = _rowptr_from_sorted(rows, U + I)
+    return rowptr, src, keys
+
+
 def split_indices(n: int, seed: int = 42, fractions=(0.8, 0.1, 0.1)):
     """Seeded 80/10/10 split of interaction indices (train, val, test)."""
     rng = np.random.default_rng(seed)

@@ -28,13 +28,20 @@ def calHammingDistance(recommendations: torch.Tensor, k: int) -> float:
 def calInternalSimilarity(recommendations: torch.Tensor, item_degree_dict: dict,
                           interaction_mat: np.ndarray, k: int) -> float:
     """Reference :66-115. interaction_mat is the binary user x item matrix of
-    getInteractionMatrixByDataframe (its column dot products are co-occurrence counts)."""
+    getInteractionMatrixByDataframe (its column dot products are co-occurrence counts), or
+    the same interactions as a user-major lgcnhs RowSets (the training loop's form: no
+    dense U x I matrix)."""
     recs = torch.as_tensor(recommendations)
     dev = gpu_device(recs)
-    A = np.asarray(interaction_mat)
-    n_items = A.shape[1]
-    if not np.all((A == 0) | (A == 1)):
-        raise ValueError("calInternalSimilarity: interaction_mat must be 0/1")
+    if isinstance(interaction_mat, RowSets):
+        n_items = interaction_mat.n_cols
+        by_item = interaction_mat.transpose()
+        A = None
+    else:
+        A = np.asarray(interaction_mat)
+        n_items = A.shape[1]
+        if not np.all((A == 0) | (A == 1)):
+            raise ValueError("calInternalSimilarity: interaction_mat must be 0/1")
     deg = np.zeros(n_items, np.int64)
     outside = set()
     for it, d in item_degree_dict.items():
@@ -44,9 +51,10 @@ def calInternalSimilarity(recommendations: torch.Tensor, item_degree_dict: dict,
             outside.add(int(it))
     if outside and np.isin(recs.cpu().numpy(), list(outside)).any():
         raise IndexError("recommended item with a degree lies outside interaction_mat")
-    users, items = np.nonzero(A)
-    by_item = RowSets.from_pairs(torch.from_numpy(items), torch.from_numpy(users), n_items,
-                                 A.shape[0], dev)
+    if A is not None:
+        users, items = np.nonzero(A)
+        by_item = RowSets.from_pairs(torch.from_numpy(items), torch.from_numpy(users),
+                                     n_items, A.shape[0], dev)
     user_num = recs.shape[0]
     if user_num * k * (k - 1) == 0:
         raise ZeroDivisionError("float division by zero")

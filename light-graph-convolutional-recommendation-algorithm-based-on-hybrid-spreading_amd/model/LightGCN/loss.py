@@ -21,18 +21,61 @@ def _sorted_keys(u: torch.Tensor, p: torch.Tensor, num_items: int) -> torch.Tens
     return keys
 
 
+REJECTION_ROUNDS = 64
+
+
+def _is_positive(u: torch.Tensor, items: torch.Tensor, keys: torch.Tensor, num_items: int):
+    q = u * num_items + items
+    if keys.numel() == 0:
+        return torch.zeros_like(q, dtype=torch.bool)
+    pos = torch.searchsorted(keys, q).clamp_max(keys.numel() - 1)
+    return keys[pos] == q
+
+
+def _exact_free_items(u: torch.Tensor, keys: torch.Tensor, num_items: int, generator=None):
+    """For each entry of ``u``: a uniform draw from the items that are NOT positives of that
+    user, by rank (the r-th free item, r uniform over the free count). Raises ValueError for
+    a user who has interacted with every item (no valid negative exists)."""
+    uu = u.to(keys.device)
+    lo = torch.searchsorted(keys, uu * num_items)
+    hi = torch.searchsorted(keys, (uu + 1) * num_items)
+    n_pos = hi - lo
+    free = num_items - n_pos
+    if bool((free <= 0).any()):
+        bad = int(uu[free <= 0][0])
+        raise ValueError(f"user {bad} has interacted with every item: no negative to sample")
+    r = (torch.rand(uu.shape, device=uu.device, generator=generator) * free).long()
+    r = torch.minimum(r, free - 1)
+    out = []
+    for t in range(uu.numel()):  # few entries: the ones rejection sampling left
+        p = (keys[int(lo[t]):int(hi[t])] - int(uu[t]) * num_items).tolist()
+        c = int(r[t])
+        for x in p:  # the c-th free item: skip every positive at or below the candidate
+            if x <= c:
+                c += 1
+            else:
+                break
+        out.append(c)
+    return torch.tensor(out, dtype=torch.int64, device=u.device)
+
+
 def _negatives(u: torch.Tensor, keys: torch.Tensor, num_items: int, generator=None):
-    """One uniform item per entry of ``u`` that is not a positive of that user (rejection
-    against the sorted (user, item) keys, on the device)."""
+    """One uniform item per entry of ``u`` that is not a positive of that user: rejection
+    against the sorted (user, item) keys on the device; entries still rejected after
+    REJECTION_ROUNDS rounds (users with few free items) are drawn exactly from their
+    complement, so a positive is never returned as a negative."""
     neg = torch.randint(0, num_items, u.shape, device=u.device, generator=generator)
-    for _ in range(64):
-        q = u * num_items + neg
-        pos = torch.searchsorted(keys, q).clamp_max(keys.numel() - 1)
-        bad = keys[pos] == q
+    bad = _is_positive(u, neg, keys, num_items)
+    for _ in range(REJECTION_ROUNDS):
         if not bool(bad.any()):
-            break
+            return neg
         neg = torch.where(bad, torch.randint(0, num_items, u.shape, device=u.device,
                                              generator=generator), neg)
+        bad = _is_positive(u, neg, keys, num_items)
+    if bool(bad.any()):
+        idx = torch.nonzero(bad).flatten()
+        neg = neg.clone()
+        neg[idx] = _exact_free_items(u[idx], keys, num_items, generator)
     return neg
 
 

@@ -274,6 +274,47 @@ def get_resource(A, W):
     return np.dot(A, W)
 
 
+def spread_rows_sparse(user_rowptr, user_items, item_rowptr, item_users, n_items: int,
+                       users, lam: float) -> np.ndarray:
+    """Rows ``users`` of F = A @ HybridS(A, getSpreadingGeneralMat(A), lam) without the
+    dense I x I matrices (model/SpreadMethod/model.py:14-27, :63-85, :88-99 restated over
+    the interaction lists, fp64): for user u, every path u -> i -> v -> j with i in items(u),
+    v in users(i), j in items(v) contributes A[v,i]/k_v to general_W[i,j]
+    (``A.T / user_degrees``, k_v == 0 -> 1), W[i,j] = general_W[i,j] / den with
+    den = k_i^(1-lam) * k_j^lam (den == 0 -> 1), and F[u,j] = sum_i W[i,j]. The sums run in
+    path order, not BLAS order (a rounding-level difference: callers compare with a
+    tolerance). Returns float64 [len(users), n_items]."""
+    urp = np.asarray(user_rowptr, np.int64)
+    uit = np.asarray(user_items, np.int64)
+    irp = np.asarray(item_rowptr, np.int64)
+    ius = np.asarray(item_users, np.int64)
+    k_u = np.diff(urp).astype(np.float64)
+    k_u[k_u == 0] = 1
+    k_i = np.diff(irp).astype(np.float64)
+    alpha = np.power(k_i, 1 - lam)
+    beta = np.power(k_i, lam)
+    out = np.zeros((len(users), n_items))
+    for r, u in enumerate(users):
+        its = uit[urp[u]:urp[u + 1]]
+        if its.size == 0:
+            continue
+        nv = irp[its + 1] - irp[its]
+        i_of = np.repeat(its, nv)
+        v_of = ius[np.concatenate([np.arange(irp[i], irp[i + 1]) for i in its])]
+        nj = urp[v_of + 1] - urp[v_of]
+        i_p = np.repeat(i_of, nj)
+        w_p = np.repeat(1.0 / k_u[v_of], nj)
+        j_p = uit[np.concatenate([np.arange(urp[v], urp[v + 1]) for v in v_of])]
+        key = i_p * n_items + j_p
+        uk, inv = np.unique(key, return_inverse=True)
+        gw = np.bincount(inv, weights=w_p)
+        ii, jj = uk // n_items, uk % n_items
+        den = alpha[ii] * beta[jj]
+        den[den == 0] = 1
+        out[r] = np.bincount(jj, weights=gw / den, minlength=n_items)
+    return out
+
+
 def spread_overrides(method: str, dataset: str, lam: float, gW: np.ndarray):
     """model/SpreadMethod/recommend.py:86-111: the lambda / transpose per method."""
     if method == "ProbS" and dataset == "movielens":

@@ -24,3 +24,39 @@ def compare_topk_sets(got, ref, gaps=None, tol=0.0, max_tie_frac=0.01):
     assert not bad, f"{len(bad)} users differ beyond ties, first: {bad[:3]}"
     assert ties <= max(1, int(max_tie_frac * ref.shape[0])), f"too many tie-affected users: {ties}"
     return ties
+
+
+def compare_topk_exact(got, ref, exact, tol, label=""):
+    """Top-k sets against a reference computed in a different rounding order, judged by
+    exact (fp64) scores. got/ref: [U, k] item ids (-1 = padding); exact(u, items) -> fp64
+    exact scores of those items for user u; tol(u, items) -> a rigorous bound on how far
+    either method's rounded score of each item can be from its exact score.
+
+    A user whose two sets differ is *tie-affected* when every item in the symmetric
+    difference has an exact score within its tolerance (plus the boundary item's) of the
+    reference's k-th exact score: some rounding within the bounds orders it either way.
+    Any other difference fails. Returns (tie-affected users, users compared) and prints
+    the count (the north_star parity claim is "identical top-K sets except rounding-level
+    ties", so the number is reported, not hidden)."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    bad, ties = [], 0
+    for u in range(ref.shape[0]):
+        g = set(got[u][got[u] >= 0].tolist())
+        r = set(ref[u][ref[u] >= 0].tolist())
+        if g == r:
+            continue
+        rl = np.array(sorted(r), np.int64)
+        er = exact(u, rl)
+        b = int(np.argmin(er))
+        eb, tb = er[b], tol(u, rl[b:b + 1])[0]
+        diff = np.array(sorted(g ^ r), np.int64)
+        ed, td = exact(u, diff), tol(u, diff)
+        if np.all(np.abs(ed - eb) <= td + tb):
+            ties += 1
+            continue
+        bad.append((u, sorted(g - r), sorted(r - g), float(np.max(np.abs(ed - eb) - td - tb))))
+    print(f"[{label}] tie-affected users: {ties} of {ref.shape[0]}")
+    assert not bad, f"{label}: {len(bad)} users differ beyond rounding ties, first: {bad[:3]}"
+    return ties, ref.shape[0]

@@ -74,7 +74,7 @@ def _worker(rank, world, port, U, I, n, k, tile, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tile", [(2, 16), (3, 7), (3, 64)])
+@pytest.mark.parametrize("world,tile", [(2, 16), (3, 7), (3, 64), (8, 5)])
 def test_sharded_spread_gloo(world, tile):
     U, I, n, k = 23, 50, 300, 6
     ctx = mp.get_context("spawn")

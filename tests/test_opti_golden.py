@@ -44,3 +44,47 @@ def test_gpu_opti_forward_matches_reference(golden, L):
     assert np.abs(uf.detach().cpu().numpy() - g[f"out_u_L{L}"]).max() <= 1e-4
     assert np.abs(itf.detach().cpu().numpy() - g[f"out_i_L{L}"]).max() <= 1e-4
     assert np.array_equal(u0.detach().cpu().numpy(), g["e0_u"])
+
+
+@pytest.mark.gpu
+def test_gpu_spread_opti_douban_matches_reference(golden, monkeypatch, tmp_path):
+    """BASELINE configs[2] (Douban-shaped SpreadLightGCNOpti, lambda = 0.5): the package's
+    recommendSpreadLightGCNOpti (fused GPU spreading + e0 scores) against the reference's
+    own getResourceMat + recommendForAllUser run (spread_opti_douban.npz,
+    make_golden_c3.py), both on the untrained seeded LightGCNOpti. Tie-aware at 1e-12 of
+    the largest boundary value (fp64 F, BLAS vs ordered sums)."""
+    import pandas as pd
+    from golden.make_golden_c3 import features
+    from const import cfg
+    from lgcnhs.synth import synth_dataframes
+    import model.SpreadLightGCNOpti.model as SM
+    from model.LightGCNOpti.model import LightGCNOpti
+    from model.SpreadLightGCNOpti.recommend import recommendSpreadLightGCNOpti
+    from _compare import compare_topk_sets
+    g = golden("spread_opti_douban")
+    U, I, E, k = int(g["n_users"]), int(g["n_items"]), int(g["n_edges"]), int(g["k"])
+    rating_df, tr, va, te = synth_dataframes(U, I, E, seed=int(g["seed"]), dist="zipf")
+    fu, fi = features(U, I)
+    uf_df = pd.DataFrame({"user_id": np.arange(U), "user_features": [list(map(float, r)) for r in fu]})
+    if_df = pd.DataFrame({"item_id": np.arange(I), "item_features": [list(map(float, r)) for r in fi]})
+
+    def untrained(user_num, item_num, edge_index, train_ei, val_ei, uf, itf, kk):
+        torch.manual_seed(42)
+        return LightGCNOpti(user_num, item_num, 64, 3, uf, itf).cuda()
+
+    monkeypatch.setattr(SM, "load_or_train_opti", untrained)
+    saved = (dict(cfg.MODEL), dict(cfg.RECOMMEND))
+    try:
+        cfg.MODEL["name"] = "SpreadLightGCNOpti"
+        cfg.MODEL["HyperParameter"] = {"lambda": float(g["lam"]), "seed": 42,
+                                       "embedding_dim": 64, "layers": 3}
+        cfg.RECOMMEND["k"] = k
+        cfg.RECOMMEND["save_path"] = str(tmp_path) + "/"
+        recs = recommendSpreadLightGCNOpti(U, I, rating_df, tr, va, te, uf_df, if_df)
+    finally:
+        cfg.MODEL.clear(); cfg.MODEL.update(saved[0])
+        cfg.RECOMMEND.clear(); cfg.RECOMMEND.update(saved[1])
+    got = np.array([recs[u] for u in range(U)])
+    gaps = g["gaps"]
+    ties = compare_topk_sets(got, g["recs"], gaps, tol=1e-12 * np.nanmax(np.abs(gaps)))
+    print(f"[C3 SpreadLightGCNOpti douban-shape] tie-affected users: {ties} of {U}")

@@ -140,3 +140,19 @@ def test_spread_lightgcn_recs(golden):
     got = np.array([recs[u] for u in range(U)])
     gaps = g["slgcn_gaps"]
     compare_topk_sets(got, g["slgcn_recs"], gaps, tol=1e-12 * np.nanmax(np.abs(gaps)))
+
+
+@pytest.mark.parametrize("lam", [0.0, 0.5, 1.0])
+def test_spread_rows_sparse_equals_dense_restatement(golden, lam):
+    """The oracle's list-based F rows (the C5-scale checker of test_gpu_configs.py) equal
+    the dense numpy restatement pinned to the reference fixtures, to fp64 rounding."""
+    g = golden("spread_ml100k")
+    U, I, A = _spread_case(g)
+    F = O.get_resource(A, O.hybrid_s(A, O.spreading_general_mat(A.copy()), lam))
+    uu, ii = np.nonzero(A)
+    urp = np.searchsorted(uu, np.arange(U + 1))
+    order = np.lexsort((uu, ii))
+    irp = np.searchsorted(ii[order], np.arange(I + 1))
+    users = np.array([0, 5, 17, U - 1])
+    Fs = O.spread_rows_sparse(urp, ii, irp, uu[order], I, users, lam)
+    np.testing.assert_allclose(Fs, F[users], rtol=1e-12, atol=1e-15 * np.abs(F).max())
