@@ -66,10 +66,31 @@ def gen_graph(U, I, E, seed, dev):
     return synth_graph_device(U, I, E, seed, dev)
 
 
-def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
+def cpu_threads():
+    """Host threads for the CPU baselines: the job's CPU share
+    (OMP_NUM_THREADS, which the GPU box sets to the CPUs it allots one job) or else
+    os.cpu_count(); set explicitly with torch.set_num_threads. Returns (threads, host CPUs,
+    CPU model)."""
+    n = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    torch.set_num_threads(n)
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, os.cpu_count(), model
+
+
+def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000, reps=5):
     """The oracle's PyG op sequence (index_select * w, index_add_) on the host cores over a
-    bounded sample: the first rows of the graph until ~target_nnz edges, full-size x."""
+    bounded sample: the first rows of the graph until ~target_nnz edges, full-size x;
+    median of `reps` after one warm-up."""
     from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
+    threads, host_cpus, model = cpu_threads()
     rp = rowptr.cpu()
     r_end = int(torch.searchsorted(rp, torch.tensor([target_nnz])).item())
     r_end = max(1, min(r_end, n))
@@ -84,36 +105,81 @@ def cpu_baseline(rowptr, src, n, dim, layers, target_nnz=4_000_000):
     w = dis[s] * dis[t]
     x = torch.randn(n, dim) * 0.1
     O.propagate(ei, w, x)  # warm-up
-    reps = []
-    for _ in range(3):
+    times = []
+    for _ in range(reps):
         t0 = time.perf_counter()
         cur = x
         for _ in range(layers):
             cur = O.propagate(ei, w, cur)
-        reps.append(time.perf_counter() - t0)
-    secs = sorted(reps)[1]
-    return {"value": e_end * layers / secs, "unit": "edge-layers/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+        times.append(time.perf_counter() - t0)
+    secs = sorted(times)[reps // 2]
+    return {"value": e_end * layers / secs, "unit": "edge-layers/s", "cores": threads,
+            "host_cpus": host_cpus, "cpu_model": model, "kind": "port",
             "sample": f"PyG op sequence (index_select*w, index_add_) over rows [0,{r_end}) = "
-                      f"{e_end} directed nnz x {layers} layers, full {n}x{dim} x, median of 3"}
+                      f"{e_end} directed nnz x {layers} layers, full {n}x{dim} x, median of "
+                      f"{reps}"}
 
 
-def cpu_baseline_topk(e0_orig, keys, U, I, k, n_users=512):
+def cpu_baseline_topk(e0_orig, keys, U, I, k, n_users=4096, block=512):
     """The reference's e0 scoring + -1024 masks + torch.topk (model/LightGCN/recommend.py:
-    83-114, restated by the oracle) on the host cores for a block of users x all items."""
+    83-114, restated by the oracle) on the host cores for a 4,096-user block x all items
+    (BASELINE.md §3), in 512-user slices (a 4,096 x 1M fp32 score matrix is 16 GB).
+    Returns the baseline line and the CPU lists (compared with the GPU's by the caller)."""
     from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
-    eu = e0_orig[:n_users].cpu()
+    threads, host_cpus, model = cpu_threads()
     ei = e0_orig[U:U + I].cpu()
-    blk = keys[keys < n_users * I].cpu()
-    pairs = (blk // I, blk % I)
-    O.recommend_topk_torch(eu[:8], ei, None, None, k)  # warm-up
-    t0 = time.perf_counter()
-    O.recommend_topk_torch(eu, ei, pairs, None, k)
-    secs = time.perf_counter() - t0
-    return {"value": n_users / secs, "unit": "recs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+    O.recommend_topk_torch(e0_orig[:8].cpu(), ei, None, None, k)  # warm-up
+    lists = []
+    secs = 0.0
+    for b0 in range(0, n_users, block):
+        b1 = min(n_users, b0 + block)
+        eu = e0_orig[b0:b1].cpu()
+        blk = keys[(keys >= b0 * I) & (keys < b1 * I)].cpu()
+        pairs = (blk // I - b0, blk % I)
+        t0 = time.perf_counter()
+        _, idx, _ = O.recommend_topk_torch(eu, ei, pairs, None, k)
+        secs += time.perf_counter() - t0
+        lists.append(idx)
+    line = {"value": n_users / secs, "unit": "recs/s", "cores": threads,
+            "host_cpus": host_cpus, "cpu_model": model, "kind": "port",
             "sample": f"torch.matmul + -1024 index-put + torch.topk(k={k}) for users "
-                      f"[0,{n_users}) x {I} items (fp32, the reference's op sequence)"}
+                      f"[0,{n_users}) x {I} items in {block}-user slices (fp32, the "
+                      f"reference's op sequence)"}
+    return line, torch.cat(lists)
+
+
+def topk_parity(gpu_idx, cpu_idx, e0_orig, U, D, k):
+    """GPU top-k lists (lg_score_topk_f32's fp32 chain) against the CPU reference op
+    sequence's (BLAS fp32) for the same users: identical sets, or tie-affected users whose
+    differing items all have exact (fp64) scores within both methods' rounding bound
+    (2 * gamma_d * sum |u_k i_k|) of the reference's k-th exact score. Returns counts."""
+    g = gpu_idx.cpu().numpy()
+    c = cpu_idx.cpu().numpy()
+    n = c.shape[0]
+    gam = 2.0 * D * 2.0 ** -24 / (1 - D * 2.0 ** -24)
+    ties = bad = 0
+    for u in range(n):
+        sg, sc = set(g[u].tolist()), set(c[u].tolist())
+        if sg == sc:
+            continue
+        eu = e0_orig[u].double().cpu()
+        items = torch.tensor(sorted(sg | sc))
+        ei = e0_orig[U + items].double().cpu()
+        ex = ei @ eu
+        tol = gam * (ei.abs() @ eu.abs())
+        pos = {int(i): t for t, i in enumerate(items.tolist())}
+        ref_ex = torch.tensor([float(ex[pos[int(i)]]) for i in c[u]])
+        b = int(torch.argmin(ref_ex))
+        eb, tb = float(ref_ex[b]), float(tol[pos[int(c[u][b])]])
+        diff = sg ^ sc
+        if all(abs(float(ex[pos[i]]) - eb) <= float(tol[pos[i]]) + tb for i in diff):
+            ties += 1
+        else:
+            bad += 1
+    return {"users": n, "k": k, "identical": n - ties - bad, "tie_affected": ties,
+            "mismatched": bad,
+            "rule": "sets equal, or every differing item's exact fp64 score within both "
+                    "methods' fp32 rounding bound of the reference's k-th exact score"}
 
 
 def cpu_baseline_spread(k, lam=0.5):
@@ -124,6 +190,7 @@ def cpu_baseline_spread(k, lam=0.5):
     import numpy as np
     from oracle import lgcn_oracle as O  # noqa: F401  (the port being timed)
     from lgcnhs.synth import synth_interactions
+    cpu_threads()
     du, di, de = 600, 20_000, 60_000
     users, items = synth_interactions(du, di, de, seed=3, dist="zipf")
     g = torch.Generator().manual_seed(42)
@@ -138,8 +205,9 @@ def cpu_baseline_spread(k, lam=0.5):
     rp = np.searchsorted(users, np.arange(du + 1))
     O.rows_topk(F, k, rp, items.astype(np.int32), True)
     secs = time.perf_counter() - t0
-    return {"value": du / secs, "unit": "recs/s", "cores": torch.get_num_threads(),
-            "kind": "port", "seconds": secs,
+    threads, host_cpus, model = cpu_threads()
+    return {"value": du / secs, "unit": "recs/s", "cores": threads, "host_cpus": host_cpus,
+            "cpu_model": model, "kind": "port", "seconds": secs,
             "sample": f"dense fp64 numpy general_W / HybridS / A@W, G*F, filtered top-{k}: "
                       f"{du} users x {di} items, {de} Zipf interactions (c3_douban_shape)"}
 
@@ -361,7 +429,7 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
                                            stats=st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    entries = float(st.get("w_entries_read", 0))
+    entries = float(st.get("w_slots_read", 0))
     if world > 1:
         e = torch.tensor([entries], dtype=torch.float64, device=dev)
         dist.all_reduce(e)
@@ -379,8 +447,8 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     del A, idx
     torch.cuda.empty_cache()
     res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
-           "path_updates_per_s": entries / dt,
-           "w_entry_GBps": entries * 12 / dt / 1e9,
+           "w_slots_per_s": entries / dt,
+           "w_slot_GBps": entries * 4 / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_tile_{seek,cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 "
@@ -415,13 +483,28 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
 
 
 def load_traffic(workload, world):
+    """roofline.traffic: HBM bytes per SpMM launch from the PMC pass recorded in
+    profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH x 2 per the
+    gfx950 correction; scripts/profile.sh + scripts/pmc_summary.py). The entry is used only
+    if the kernel source it was measured on (sha256 of csrc/spmm.hip) is the one built now;
+    otherwise traffic is null and the reason is reported."""
+    import hashlib
+    src = os.path.join(PKG, "csrc", "spmm.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        e = d.get(f"{workload}/n{world}")
-        return None if e is None else float(e["hbm_bytes_per_launch"])
     except Exception:
-        return None
+        return None, {"status": "no PMC record", "kernel_sha": sha}
+    e = d.get(f"{workload}/n{world}")
+    if e is None:
+        return None, {"status": f"no PMC record for {workload}/n{world}", "kernel_sha": sha}
+    if e.get("kernel_sha") != sha:
+        return None, {"status": "stale: recorded on another spmm.hip",
+                      "recorded_sha": e.get("kernel_sha"), "kernel_sha": sha,
+                      "source": e.get("source")}
+    return float(e["hbm_bytes_per_launch"]), {"status": "measured", "kernel_sha": sha,
+                                               "source": e.get("source")}
 
 
 def main():
@@ -516,7 +599,7 @@ def main():
     alg_bytes = shard.nnz * (8 + 4 * D) + shard.n_rows * (4 + 4 * D)
     achieved = alg_bytes / avg_kernel_s / 1e9
     job_bytes = nnz * (8 + 4 * D) + N * (4 + 4 * D)  # one layer of the whole graph
-    traffic = load_traffic(args.workload, world)
+    traffic, traffic_src = load_traffic(args.workload, world)
 
     # the same graph at the other embedding widths the configs name (C5: d=128)
     extra = {}
@@ -543,7 +626,7 @@ def main():
         del train_graph
         torch.cuda.empty_cache()
 
-    topk = None
+    topk = topk_gpu_lists = None
     if not args.no_topk:
         nu = min(args.topk_users, U)
         u0 = (rank * nu) % max(1, U - nu + 1)
@@ -570,6 +653,7 @@ def main():
                 "ms": tk * 1e3, "tflops_per_gpu": flops / tk / 1e12,
                 "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
                 "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
+        topk_gpu_lists = ops.score_topk(eu, ei, args.k, excl)[1] if u0 == 0 else None
 
     spread = None
     if not args.no_spread:
@@ -589,7 +673,11 @@ def main():
     if cpu_src is not None:
         try:
             cpu = cpu_baseline(cpu_rp, cpu_src, N, D, L)
-            cpu_topk = cpu_baseline_topk(e0_orig, keys, U, I, args.k)
+            cpu_topk, cpu_lists = cpu_baseline_topk(e0_orig, keys, U, I, args.k)
+            if topk is not None and topk_gpu_lists is not None:
+                n_cmp = min(cpu_lists.shape[0], topk_gpu_lists.shape[0])
+                topk["parity_vs_cpu_reference"] = topk_parity(
+                    topk_gpu_lists[:n_cmp], cpu_lists[:n_cmp], e0_orig, U, D, args.k)
             cpu_spread = cpu_baseline_spread(args.k)
         except Exception as ex:  # the baseline must never hide the GPU result
             log(f"cpu baseline failed: {ex!r}")
@@ -607,7 +695,8 @@ def main():
                                          if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": "lg_spmm_layer_f32",
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "lg_spmm_layer_f32",
                          "avg_launch_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes,
                          # north_star's end-to-end figure: value (all ranks, all-gathers

@@ -238,34 +238,42 @@ int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
                          int64_t n_items, const uint16_t *count, int64_t *bound,
                          lg_stream_t stream);
 
-/* Row i of W restricted to the tile, for every item i:
- *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} inv_deg[v])
- *             / (alpha[i] * beta[j])          (den == 0 -> 1)
- * written in ascending j as 12-byte entries {int32 j; fp64 value, 4-byte aligned} at
- * wt_ent[wt_ptr[i] .. wt_ptr[i] + len_i), where wt_ptr[n_items + 1] is the exclusive prefix
- * of the row capacities: lg_spread_tile_bound's bounds, or the bounds rounded up to a
- * multiple m of entries with 256 % m == 0 (rows then start m*12 bytes apart: m = 32 puts
- * every row on a 128-B line; a capacity above 256 still means exactly a bound above 256,
- * the block-per-row path), and wt_meta[i] = wt_ptr[i] |
- * (len_i << 48) (one 8-byte lookup per row for the resource pass); cur/count from
- * lg_spread_tile_cursor, inv_deg from lg_inv_degree_f64 over the user rows. ws:
- * lg_spread_tile_weight_ws_bytes(n_items) bytes of scratch. tile in [1, 8192]; every item
- * of the tile must lie in [item_begin, item_begin + tile). */
+/* Row i of W restricted to the tile, for every item i, where
+ *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} fl(1/k_v))
+ *             / (alpha[i] * beta[j])          (den == 0 -> 1),
+ * stored at wt_ent[wt_ptr[i] ..] (4-byte slots) in one of two formats:
+ *   P rows (bound[i] <= 256 pairs): one slot per (user v, item j) pair, sorted by (j, v):
+ *     bits 0-15 j - item_begin, bits 16-29 user_cls[v] (the class of v's degree:
+ *     inv_cls[user_cls[v]] = fl(1/k_v)), bit 30 "next slot same column", bit 31 "previous
+ *     slot same column"; the walk forms each path's W value from these (same bits);
+ *   V rows (hub items, bound[i] > 256): one 12-byte triple per distinct column,
+ *     {(0x3FFF << 16) | (j - item_begin), fp64 W value as lo, hi}.
+ * wt_meta[i] = {ptr | len << 40 | V << 63, alpha[i]} (16 bytes; len in slots). wt_ptr is
+ * the caller's prefix of row capacities (in slots): bound[i] for P rows,
+ * 3 * min(bound[i], tile) for V rows, each rounded up to a multiple of 32 slots so rows
+ * start on 128-byte lines. cur/count from lg_spread_tile_cursor, bound from
+ * lg_spread_tile_bound, inv_deg from lg_inv_degree_f64 over the user rows (V rows), user_cls
+ * one uint16 class per user (< 16383 classes). ws: lg_spread_tile_weight_ws_bytes(n_items)
+ * bytes of scratch. tile in [1, 8192]; every item of the tile lies in
+ * [item_begin, item_begin + tile). */
 size_t lg_spread_tile_weight_ws_bytes(int64_t n_items);
 int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                              const int32_t *user_items, const double *inv_deg,
-                              int64_t n_items, const int64_t *cur, const uint16_t *count,
-                              const double *alpha, const double *beta, int32_t item_begin,
-                              int32_t tile, const int64_t *wt_ptr, void *wt_ent,
-                              uint64_t *wt_meta, void *ws, size_t ws_bytes,
-                              lg_stream_t stream);
+                              const int32_t *user_items, const uint16_t *user_cls,
+                              const double *inv_deg, int64_t n_items, const int64_t *cur,
+                              const uint16_t *count, const double *alpha, const double *beta,
+                              int32_t item_begin, int32_t tile, const int64_t *bound,
+                              const int64_t *wt_ptr, void *wt_ent, void *wt_meta, void *ws,
+                              size_t ws_bytes, lg_stream_t stream);
 
 /* F[u][j - item_begin] = sum_{i in items(u), ascending} W[i][j] for the n_users rows of
- * user_rowptr (pass user_rowptr + u0 for a block) and j in [item_begin, item_begin + tile);
- * F row-major with leading dim ldf >= tile; wt_meta / wt_ent from lg_spread_tile_weight_f64. */
+ * user_rowptr (pass user_rowptr + u0 for a block) and j in [item_begin, item_begin + tile)
+ * (columns >= item_begin + width are 0); F row-major with leading dim ldf >= tile;
+ * wt_meta / wt_ent from lg_spread_tile_weight_f64, beta = all items' beta, inv_cls the
+ * degree-class table. */
 int lg_spread_tile_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                int64_t n_users, const uint64_t *wt_meta, const void *wt_ent,
-                                int32_t item_begin, int32_t tile, double *F, int64_t ldf,
+                                int64_t n_users, const void *wt_meta, const void *wt_ent,
+                                const double *beta, const double *inv_cls, int32_t item_begin,
+                                int32_t tile, int32_t width, double *F, int64_t ldf,
                                 lg_stream_t stream);
 
 /* Merge columns [item_begin, item_begin + n_cols) of (G *) F (F[r][0..n_cols), leading dim
@@ -298,22 +306,37 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
  * [item_begin, item_begin + width) are accumulated in LDS (same values, bit for bit) and
  * merged straight into the running top-K lists io_val/io_idx [n_users][k] (first != 0:
  * start empty); F is never written to memory. G factor: eu = the rows' user embeddings,
- * ei = all item embeddings, item_norm = lg_row_norms_f64(ei) (|G| <= ||u|| ||i|| bounds the
- * chain, so columns that cannot beat the K-th value skip the score). Exclusions (dropped):
- * ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row cursor ex_cur[n_users] positioned
- * at the walk's first item by lg_spread_tile_seek(ex_rowptr, ex_col, ...) and advanced here.
- * Walked over tiles in ascending order, the lists equal lg_rows_topk_f64 over the full rows.
- * k in [1, 128]; dim in {32, 64, 128}; LDS per 2-wave block:
- * lg_spread_tile_resource_topk_lds_bytes(tile, k, dim or 0). */
+ * ei = all item embeddings, gb = lg_score_chunk_bound's [n_users][n_chunks] bounds for this
+ * tile (n_chunks = ceil(width / 64)): only columns with gb * F > the K-th value get the exact
+ * score chain. Exclusions (dropped): ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row
+ * cursor ex_cur[n_users] positioned at the walk's first item by
+ * lg_spread_tile_seek(ex_rowptr, ex_col, ...) and advanced here. Walked over tiles in
+ * ascending order, the lists equal lg_rows_topk_f64 over the full rows. k in [1, 128]; dim
+ * in {32, 64, 128}. lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
+ * workgroup's tables (the launch fits as many waves per CU as the LDS holds). */
 size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
 int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                     int64_t n_users, const uint64_t *wt_meta,
-                                     const void *wt_ent, int32_t item_begin, int32_t tile,
-                                     int32_t width, const float *eu, const float *ei,
-                                     int32_t dim, const double *item_norm,
+                                     int64_t n_users, const void *wt_meta, const void *wt_ent,
+                                     const double *beta, const double *inv_cls,
+                                     int32_t item_begin, int32_t tile, int32_t width,
+                                     const float *eu, const float *ei, int32_t dim,
+                                     const float *gb, int32_t n_chunks,
                                      const int64_t *ex_rowptr, const int32_t *ex_col,
                                      int64_t *ex_cur, int32_t k, int32_t first,
                                      double *io_val, int64_t *io_idx, lg_stream_t stream);
+
+/* x_bf16[r] = bf16(x[r]) (round to nearest even), norm_up[r] = ||x[r]||_2 rounded up to
+ * fp32: the operands of lg_score_chunk_bound (csrc/gbound.hip). */
+int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
+                      float *norm_up, lg_stream_t stream);
+
+/* gb[u][c] (fp32, [n_users][ceil(width / 64)]) >= the fp32 score chain e0_u . e0_j of every
+ * column j of chunk c = [item_begin + 64c, item_begin + 64c + 64) of the tile: the bf16 MFMA
+ * product's chunk maximum plus a rigorous rounding margin (csrc/gbound.hip). u/i from
+ * lg_bound_prep_f32 of the users' rows and of all items. dim in {32, 64, 128}. */
+int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
+                         const void *i_bf16, const float *i_norm, int32_t dim,
+                         int32_t item_begin, int32_t width, float *gb, lg_stream_t stream);
 
 /* out[r] = ||x[r]||_2 (fp64) for an fp32 [n_rows, dim] matrix. */
 int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,

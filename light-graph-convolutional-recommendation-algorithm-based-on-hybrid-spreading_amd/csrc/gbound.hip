@@ -1,0 +1,157 @@
+// Score bounds for the LGCNHS top-K walk (SURVEY.md §8 a9-a12 at C5): for every user u and
+// 64-column chunk c of an item tile, gb[u][c] >= the fp32 chain score G(u, j) =
+// e0_u . e0_j (model/SpreadLightGCN/model.py:74-77, the chain of lg_score_topk_f32) of
+// every column j of the chunk. The walk (lg_spread_tile_resource_topk_f64) computes the
+// exact chain only for columns whose gb * F can beat the user's K-th value.
+//
+// The bound is a bf16 MFMA product plus a rigorous margin. With the operands rounded to
+// bf16 (relative error <= 2^-8 each) and an fp32-accumulated dot product of 64..128 terms,
+//   |G_bf16 - G_chain| <= sum_k |u_k j_k| (2^-7 + 2^-16 + 2 gamma_D (1 + 2^-7))
+//                      <= 0.00785 ||u|| ||j||           (gamma_128 = 128 * 2^-24)
+// so gb = max_{j in c} G_bf16 + 0.008 ||u|| max_{j in c} ||j|| (norms rounded up to fp32),
+// nudged up by 2^-22 relative for the fp32 operations that formed it, is an upper bound.
+// Then fl(G_chain * F) <= fl(gb * F) for every F >= 0 (rounding is monotone), so a column
+// with gb * F <= tau can not beat tau. Cost per tile: 2 * U * T * D flop on bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16: 16 items x 16 users x 32 dims per instruction; 64 users per
+// wave share every item fragment).
+#include <math.h>
+
+#include "common.h"
+
+namespace lg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float kBoundMargin = 0.008f;
+
+__device__ __forceinline__ float round_up_f32(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, __builtin_huge_valf());
+  return f;
+}
+
+// xb[r] = bf16(x[r]) (round to nearest even), norm[r] = ||x[r]||_2 rounded up to fp32.
+// One wave per row.
+__global__ __launch_bounds__(256) void k_bound_prep(const float *__restrict__ x, int64_t n,
+                                                    int dim, __bf16 *__restrict__ xb,
+                                                    float *__restrict__ norm) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (r >= n) return;
+  const int lane = lane_id();
+  double ss = 0.0;
+  for (int d = lane; d < dim; d += 64) {
+    const float v = x[r * dim + d];
+    xb[r * dim + d] = (__bf16)v;
+    ss += (double)v * (double)v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  // sqrt of an fp64 sum of squares of fp32 values: relative error ~1e-16, far below the
+  // fp32 round-up (the margin constant leaves 2 % slack besides)
+  if (lane == 0) norm[r] = round_up_f32(sqrt(ss) * (1.0 + 1e-12));
+}
+
+// One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile.
+template <int D>
+__global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ ub,
+                                                     const float *__restrict__ unorm,
+                                                     int64_t n_users,
+                                                     const __bf16 *__restrict__ ib,
+                                                     const float *__restrict__ inorm,
+                                                     int32_t item_begin, int32_t width,
+                                                     int32_t nch, float *__restrict__ gb) {
+  constexpr int S = D / 32;  // k-steps
+  const int lane = lane_id();
+  const int64_t ubase = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 64;
+  if (ubase >= n_users) return;
+  const int ul = lane & 15, kg = lane >> 4;
+  bf16x8 bfr[4][S];
+  float un[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    int64_t uu = ubase + 16 * g + ul;
+    uu = uu < n_users ? uu : n_users - 1;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      bfr[g][s] = *reinterpret_cast<const bf16x8 *>(ub + uu * D + 32 * s + 8 * kg);
+    un[g] = unorm[uu];
+  }
+  for (int c = 0; c < nch; ++c) {
+    const int cb = 64 * c;  // chunk start inside the tile
+    // the chunk's largest item norm (wave-uniform)
+    float inm = cb + lane < width ? inorm[item_begin + cb + lane] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) inm = fmaxf(inm, __shfl_xor(inm, o));
+    float gmax[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gmax[g] = -__builtin_huge_valf();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      int it = cb + 16 * t + ul;  // A row = item
+      it = it < width ? it : width - 1;
+      bf16x8 afr[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        afr[s] = *reinterpret_cast<const bf16x8 *>(ib + (int64_t)(item_begin + it) * D +
+                                                  32 * s + 8 * kg);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[s], bfr[g][s], acc, 0, 0, 0);
+        // lane holds rows (items) 4*kg + r of this 16-item tile, column (user) ul
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cb + 16 * t + 4 * kg + r < width) gmax[g] = fmaxf(gmax[g], acc[r]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float m = gmax[g];
+      m = fmaxf(m, __shfl_xor(m, 16));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      float b = m + kBoundMargin * un[g] * inm;
+      b += fabsf(b) * 0x1p-22f + 1e-30f;
+      const int64_t uu = ubase + 16 * g + ul;
+      if (kg == 0 && uu < n_users) gb[uu * nch + c] = b;
+    }
+  }
+}
+
+}  // namespace lg
+
+using namespace lg;
+
+extern "C" int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
+                                 float *norm_up, lg_stream_t stream) {
+  LG_REQUIRE(x && x_bf16 && norm_up && n_rows >= 0 && dim >= 1,
+             "lg_bound_prep_f32: bad arguments");
+  if (n_rows == 0) return LG_OK;
+  k_bound_prep<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
+      x, n_rows, dim, (__bf16 *)x_bf16, norm_up);
+  return launch_status("lg_bound_prep_f32");
+}
+
+extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
+                                    const void *i_bf16, const float *i_norm, int32_t dim,
+                                    int32_t item_begin, int32_t width, float *gb,
+                                    lg_stream_t stream) {
+  LG_REQUIRE(u_bf16 && u_norm && i_bf16 && i_norm && gb && n_users >= 0 && item_begin >= 0 &&
+                 width >= 1,
+             "lg_score_chunk_bound: bad arguments");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_chunk_bound: dim %d not in "
+             "{32,64,128}", dim);
+  if (n_users == 0) return LG_OK;
+  const int nch = (width + 63) / 64;
+  const dim3 grid((unsigned)((n_users + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  const __bf16 *u = (const __bf16 *)u_bf16, *i = (const __bf16 *)i_bf16;
+  switch (dim) {
+    case 32: k_chunk_bound<32><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
+    case 64: k_chunk_bound<64><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
+    default: k_chunk_bound<128><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
+  }
+  return launch_status("lg_score_chunk_bound");
+}

@@ -12,22 +12,18 @@
 //   cursor   end[v] = first position of user v's (ascending) item row with item >= j0 + T;
 //            cur[v] (the previous tile's end) marks the first item >= j0, so
 //            items(v) inside the tile = user_items[cur[v] .. end[v])
-//   bound    bound[i] = sum_{v in users(i)} (end[v] - cur[v]) >= entries of W's row i in
-//            the tile; the caller's exclusive prefix of it is wt_ptr (row capacities)
-//   weight   row i of W restricted to the tile: the (item j, user v) pairs of all
-//            v in users(i) sorted by (j, v) in one wave (bitonic, <= 256 pairs), each run
-//            of equal j summed in ascending v, divided by alpha[i] * beta[j]. Rows with
-//            more than 256 pairs (hub items) go through a block-wide dense LDS tile with
-//            the users walked in ascending order. Either way the value is, bit for bit,
-//            lg_spread_general_f64's sum (ascending v, fl(1/k_v)) / lg_hybrid_weight_f64's
-//            den, so the tiled path equals the dense one exactly.
-//   resource F[u][j - j0] = sum_{i in items(u), ascending} W[i][j]: one wave per user, the
-//            tile's accumulator in LDS; row i's entries are distinct columns, so rows are
-//            added one after another without atomics (lg_spread_resource_f64's order).
-//   topk     the tile's columns of (G *) F merged into running per-user top-K lists
-//            (G = e0 score by f32 MFMA, the chain of lg_score_topk_f32, promoted to fp64).
+//   bound    bound[i] = sum_{v in users(i)} (end[v] - cur[v]) = the (user, item) pairs
+//            behind row i of W in the tile
+//   weight   row i of W restricted to the tile (format below: the pairs themselves, 4 bytes
+//            each, for ordinary rows; merged fp64 values for hub rows)
+//   walk     per user: F[u][j - j0] = sum_{i in items(u), ascending} W[i][j] in an LDS
+//            accumulator (one wave per user, lg_spread_resource_f64's order and values), then
+//            either written out (F mode) or merged straight into the user's running top-K
+//            list (top-K mode: (G *) F, G = the fp32 e0 score chain, candidates screened by
+//            per-(user, 64-column chunk) score bounds from lg_score_chunk_bound).
 // Work: the weight pass costs sum_i deg(i) lookups + the 2-hop pairs once per tile (not per
-// user); the resource pass reads deg(u) short row segments per user and tile.
+// user); the walk reads deg(u) short row segments per user and tile (~1e12 paths at C5:
+// 4 bytes per path, F never leaves LDS).
 #include <stdlib.h>
 
 #include "common.h"
@@ -36,21 +32,39 @@ namespace lg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// One entry of a W tile row: 12 bytes, {item, fp64 value as two dwords} (4-byte aligned, so
-// a row of n entries is 12n contiguous bytes: fewer 128-B lines per random row than split
-// column / value arrays). meta[i] = (row start) | (row length << 48).
-struct WEnt {
-  int32_t col;
-  uint32_t lo, hi;
-};
-constexpr int kMetaShift = 48;
-constexpr uint64_t kMetaPtrMask = (1ull << kMetaShift) - 1;
+// A W tile is stored as one row segment per item i, in one of two formats (RowMeta, one
+// 16-byte load per row: m = ptr | len << 40 | V << 63, and alpha_i):
+//
+// P rows (<= kSortMax pairs, the common case): one 4-byte slot per (user v, item j) PAIR
+//   behind the row (v in users(i), j in items(v) inside the tile), sorted by (j, v):
+//     bits 0-15  j - item_begin
+//     bits 16-29 the class of v's degree k_v (fl(1 / k_v) = inv[class], classes < kInvTab
+//                cached in LDS)
+//     bit 30     the next slot is the same column (a run of users of one (i, j))
+//     bit 31     this slot continues the previous slot's column
+//   The resource pass forms W[i][j] = (sum of the run's fl(1/k_v), ascending v) /
+//   (alpha_i * beta_j) per path: the sum of lg_spread_general_f64 and the division of
+//   lg_hybrid_weight_f64, bit for bit, without storing an fp64 per entry (4 bytes per path
+//   instead of 12; the path count, ~1e12 at C5, sets the runtime).
+// V rows (hub items, > kSortMax pairs, merged while building): one 12-byte triple per
+//   distinct column: slot 0 = (kClsV << 16) | (j - item_begin), slots 1-2 = the fp64
+//   general_W[i][j] (lo, hi), divided by alpha_i * beta_j in the walk like a P run.
+// Neither format depends on lambda (only RowMeta's alpha and the walk's beta table do), so
+// a lambda sweep reuses the built tiles.
+constexpr uint32_t kClsMask = 0x3FFF;
+constexpr uint32_t kClsV = 0x3FFF;         // class field of a V-row triple's first slot
+constexpr uint32_t kHasNext = 0x40000000u;
+constexpr uint32_t kIsCont = 0x80000000u;
+constexpr int kLenShift = 40;
+constexpr uint64_t kPtrMask = (1ull << kLenShift) - 1;
+constexpr uint64_t kLenMask = (1ull << 23) - 1;
+constexpr uint64_t kFmtV = 1ull << 63;
+constexpr int kInvTab = 512;  // degree classes whose fl(1/k) is cached in LDS
 
-__device__ __forceinline__ void put_ent(WEnt *__restrict__ ent, int64_t pos, int32_t col,
-                                        double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  ent[pos] = WEnt{col, (uint32_t)b, (uint32_t)(b >> 32)};
-}
+struct RowMeta {
+  uint64_t m;
+  double alpha;
+};
 
 __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
                                                         int64_t n, double lambda,
@@ -127,16 +141,14 @@ __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ 
   if (lane == 0) bound[i] = s;
 }
 
-constexpr int kSortMax = 256;  // pairs per row handled by the in-wave sort
+constexpr int kSortMax = 256;  // pairs per row handled by the in-wave sort (P rows)
 
 // Sort the n (<= 64*M) staged pairs (key = -item, id = staging position, which ascends
-// with the user) of this wave, then reduce runs of equal items in ascending user order
-// (weights sw[position] = fl(1/k_v)) and write the row.
+// with the user) of this wave by (item, user) and write them as P slots.
 template <int M>
-__device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, const double *sw, int n,
-                                               int64_t wbase, double alpha_i,
-                                               const double *__restrict__ beta,
-                                               WEnt *__restrict__ wt_ent) {
+__device__ __forceinline__ void sort_write_row(int *skey, int *sid, const uint16_t *scls, int n,
+                                               int64_t wbase, int32_t item_begin,
+                                               uint32_t *__restrict__ wt_ent) {
   const int lane = lane_id();
   int k[M], id[M];
 #pragma unroll
@@ -155,49 +167,39 @@ __device__ __forceinline__ int sort_reduce_row(int *skey, int *sid, const double
     sid[e] = id[j];
   }
   wave_sync();
-  int base = 0;
 #pragma unroll
   for (int j = 0; j < M; ++j) {
     const int e = j * 64 + lane;
-    const bool head = e < n && (e == 0 || skey[e] != skey[e - 1]);
-    const uint64_t hb = __ballot(head);
-    if (head) {
-      // run e, e+1, ... of one item, users ascending: 0.0 + w0 + w1 + ... in that order
-      const int item = -skey[e];
-      double s = 0.0;
-      for (int m = e; m < n && skey[m] == skey[e]; ++m) s += sw[sid[m]];
-      double den = alpha_i * beta[item];
-      if (den == 0.0) den = 1.0;
-      const int pos = base + __popcll(hb & lanemask_lt());
-      put_ent(wt_ent, wbase + pos, item, s / den);
+    if (e < n) {
+      const int key = skey[e];
+      const bool prv = e > 0 && skey[e - 1] == key;
+      const bool nxt = e + 1 < n && skey[e + 1] == key;
+      wt_ent[wbase + e] = (prv ? kIsCont : 0u) | (nxt ? kHasNext : 0u) |
+                          ((uint32_t)scls[sid[e]] << 16) | (uint32_t)(-key - item_begin);
     }
-    base += __popcll(hb);
   }
-  return base;
 }
 
-// one wave per item row; LDS staging of kSortMax pairs per wave
+// P rows: one wave per item row with bound[i] <= kSortMax pairs (LDS staging per wave).
 __global__ __launch_bounds__(256) void k_tile_weight(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
-    const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
+    const int32_t *__restrict__ user_items, const uint16_t *__restrict__ user_cls,
     int64_t n_items, const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
-    const double *__restrict__ alpha, const double *__restrict__ beta,
-    const int64_t *__restrict__ wt_ptr, WEnt *__restrict__ wt_ent,
-    uint64_t *__restrict__ wt_meta) {
+    const double *__restrict__ alpha, int32_t item_begin, const int64_t *__restrict__ bound,
+    const int64_t *__restrict__ wt_ptr, uint32_t *__restrict__ wt_ent,
+    RowMeta *__restrict__ wt_meta) {
   __shared__ int skey[4][kSortMax];
   __shared__ int sid[4][kSortMax];
-  __shared__ double sw[4][kSortMax];
+  __shared__ uint16_t scls[4][kSortMax];
   const int wave = threadIdx.x / 64;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   if (i >= n_items) return;
   const int lane = lane_id();
+  const int64_t nb = bound[i];
+  if (nb > kSortMax) return;  // hub row: k_tile_weight_hub
   const int64_t wbase = wt_ptr[i];
-  const int64_t bound = wt_ptr[i + 1] - wbase;
-  if (bound == 0) {
-    if (lane == 0) wt_meta[i] = (uint64_t)wbase;
-    return;
-  }
-  if (bound > kSortMax) return;  // hub row: k_tile_weight_hub
+  if (lane == 0) wt_meta[i] = RowMeta{(uint64_t)wbase | ((uint64_t)nb << kLenShift), alpha[i]};
+  if (nb == 0) return;
   // stage the pairs: users of i in ascending order, each user's items inside the tile
   int n = 0;
   for (int64_t e0 = item_rowptr[i]; e0 < item_rowptr[i + 1]; e0 += 64) {
@@ -208,7 +210,6 @@ __global__ __launch_bounds__(256) void k_tile_weight(
       v = item_users[e];
       c = count[v];
     }
-    // exclusive prefix of c over the lanes
     int pre = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -219,41 +220,36 @@ __global__ __launch_bounds__(256) void k_tile_weight(
     pre -= c;
     if (c) {
       const int64_t s0 = cur[v];
-      const double w = inv_deg[v];
+      const uint16_t cl = user_cls[v];
       for (int q = 0; q < c; ++q) {
         const int p = n + pre + q;
         skey[wave][p] = -user_items[s0 + q];
         sid[wave][p] = p;
-        sw[wave][p] = w;
+        scls[wave][p] = cl;
       }
     }
     n += total;
   }
   wave_sync();
-  int len;
   if (n <= 64)
-    len = sort_reduce_row<1>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_ent);
+    sort_write_row<1>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
   else if (n <= 128)
-    len = sort_reduce_row<2>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_ent);
+    sort_write_row<2>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
   else
-    len = sort_reduce_row<4>(skey[wave], sid[wave], sw[wave], n, wbase, alpha[i], beta,
-                             wt_ent);
-  if (lane == 0) wt_meta[i] = (uint64_t)wbase | ((uint64_t)len << kMetaShift);
+    sort_write_row<4>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
 }
 
-// Hub rows (> kSortMax pairs): one 256-thread block per row (grid-stride over the hub list),
-// the tile as a dense LDS accumulator, users walked in ascending order as in
-// k_spread_general.
+// V rows (bound > kSortMax pairs, hub items): one 256-thread block per row (grid-stride
+// over the hub list), the tile as a dense LDS accumulator, users walked in ascending order
+// as in k_spread_general, then the touched columns written as merged triples.
 __global__ __launch_bounds__(256) void k_tile_weight_hub(
     const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
     const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
     const double *__restrict__ alpha, const double *__restrict__ beta, int32_t item_begin,
-    int32_t tile, const int64_t *__restrict__ wt_ptr, WEnt *__restrict__ wt_ent,
-    uint64_t *__restrict__ wt_meta) {
+    int32_t tile, const int64_t *__restrict__ wt_ptr, uint32_t *__restrict__ wt_ent,
+    RowMeta *__restrict__ wt_meta) {
   extern __shared__ double acc[];  // tile doubles
   __shared__ int wsum[4];
   const int64_t nh = *n_hub;
@@ -287,41 +283,58 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
         total += wsum[q];
       }
       if (nz) {
-        const int item = item_begin + j;
-        double den = a * beta[item];
-        if (den == 0.0) den = 1.0;
-        const int pos = base + before_w + __popcll(b & lanemask_lt());
-        put_ent(wt_ent, wbase + pos, item, acc[j] / den);
+        const uint64_t bits = (uint64_t)__double_as_longlong(acc[j]);
+        const int64_t p = wbase + 3 * (int64_t)(base + before_w + __popcll(b & lanemask_lt()));
+        wt_ent[p] = (kClsV << 16) | (uint32_t)j;
+        wt_ent[p + 1] = (uint32_t)bits;
+        wt_ent[p + 2] = (uint32_t)(bits >> 32);
       }
       base += total;
       __syncthreads();
     }
-    if (threadIdx.x == 0) wt_meta[i] = (uint64_t)wbase | ((uint64_t)base << kMetaShift);
+    if (threadIdx.x == 0)
+      wt_meta[i] = RowMeta{(uint64_t)wbase | ((uint64_t)(3 * base) << kLenShift) | kFmtV, a};
     __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ wt_ptr,
+__global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ bound,
                                                   int64_t n_items,
                                                   unsigned long long *__restrict__ n_hub,
                                                   int64_t *__restrict__ hub_rows) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
-  if (wt_ptr[i + 1] - wt_ptr[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
+  if (bound[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
 }
 
-// Resource pass (F = A W over one tile): rows of 128 items per group, see k_tile_resource.
+// ------------------------------------------------------------------ the resource pass
+// F[u][j] = sum over items(u) ascending of W[i][j]: one wave per user, the tile's
+// accumulator in LDS. A user's rows are taken 128 at a time: their RowMeta is fetched in one
+// round trip and indexed in LDS (empty rows dropped, inclusive slot prefix, slot base,
+// alpha_i); the rows' slots are then flattened: lane l takes slots e = e0 + q*64 + l of the
+// concatenated rows, UF loads in flight per lane, its row found by a short scan from the
+// previous register's last row (rows are non-empty, so 64 slots span at most 64 rows). Each
+// path's W value is formed in registers and added with ds_add_f64; adds of one instruction
+// that hit the same column come from rows in lane order and instructions go in slot order,
+// so each column receives its rows' values in ascending row order: the order of
+// lg_spread_resource_f64, hence the same bits.
 constexpr int kResRows = 128;
-constexpr int kResIdxBytes = kResRows * (4 + 8);
+struct RowIndex {
+  int cincl[kResRows];     // inclusive prefix of the rows' 4-slot chunks
+  int cexcl[kResRows];     // exclusive prefix
+  int len[kResRows];       // slots | 0x80000000 for V rows
+  int pad_[kResRows];
+  int64_t base[kResRows];  // the row's first slot
+  double alpha[kResRows];
+};
 
-// Prefix of a 128-row group's metadata (rows' entry counts and starts) into the wave's
-// row index `idx`; returns the group's total entry count.
-__device__ __forceinline__ int write_row_index(char *idx, uint64_t m0, uint64_t m1) {
+// Index of a group of up to 128 rows (RowMeta of rows lane and 64 + lane), empty rows
+// dropped; returns the group's chunk count.
+__device__ __forceinline__ int write_row_index(RowIndex *ix, RowMeta m0, RowMeta m1) {
   const int lane = lane_id();
-  int64_t *s_base = reinterpret_cast<int64_t *>(idx);
-  int *s_incl = reinterpret_cast<int *>(idx + kResRows * 8);
-  const int rl0 = (int)(m0 >> kMetaShift), rl1 = (int)(m1 >> kMetaShift);
-  int in0 = rl0, in1 = rl1;
+  const int l0 = (int)((m0.m >> kLenShift) & kLenMask), l1 = (int)((m1.m >> kLenShift) & kLenMask);
+  const int c0 = (l0 + 3) >> 2, c1 = (l1 + 3) >> 2;
+  int in0 = c0, in1 = c1;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y0 = __shfl_up(in0, o), y1 = __shfl_up(in1, o);
@@ -329,174 +342,164 @@ __device__ __forceinline__ int write_row_index(char *idx, uint64_t m0, uint64_t 
   }
   in1 += __shfl(in0, 63);
   const int total = __shfl(in1, 63);
+  const uint64_t b0 = __ballot(l0 > 0), b1 = __ballot(l1 > 0);
+  const int p0 = __popcll(b0 & lanemask_lt());
+  const int p1 = __popcll(b0) + __popcll(b1 & lanemask_lt());
   wave_sync();  // earlier readers of this index are done
-  s_incl[lane] = in0;
-  s_incl[64 + lane] = in1;
-  s_base[lane] = (int64_t)(m0 & kMetaPtrMask) - (in0 - rl0);
-  s_base[64 + lane] = (int64_t)(m1 & kMetaPtrMask) - (in1 - rl1);
+  ix->cincl[lane] = 0x7fffffff;  // rows past the group's last (binary search sentinel)
+  ix->cincl[64 + lane] = 0x7fffffff;
+  wave_sync();
+  if (l0 > 0) {
+    ix->cincl[p0] = in0;
+    ix->cexcl[p0] = in0 - c0;
+    ix->len[p0] = l0 | ((int64_t)m0.m < 0 ? (int)0x80000000 : 0);
+    ix->base[p0] = (int64_t)(m0.m & kPtrMask);
+    ix->alpha[p0] = m0.alpha;
+  }
+  if (l1 > 0) {
+    ix->cincl[p1] = in1;
+    ix->cexcl[p1] = in1 - c1;
+    ix->len[p1] = l1 | ((int64_t)m1.m < 0 ? (int)0x80000000 : 0);
+    ix->base[p1] = (int64_t)(m1.m & kPtrMask);
+    ix->alpha[p1] = m1.alpha;
+  }
   wave_sync();
   return total;
 }
 
-// acc[j - item_begin] += the `total` flattened entries of one indexed row group.
-template <int UF>
-__device__ __forceinline__ void accumulate_group(double *acc, const char *idx, int total,
-                                                 const WEnt *__restrict__ wt_ent,
-                                                 int32_t item_begin) {
+__device__ __forceinline__ double inv_of(uint32_t x, const double *s_inv,
+                                         const double *__restrict__ g_inv) {
+  const uint32_t c = (x >> 16) & kClsMask;
+  return c < kInvTab ? s_inv[c] : g_inv[c];
+}
+
+// acc[j - item_begin] += the `total` flattened 4-slot chunks of one indexed row group.
+// Lane l loads chunk c0 + 64q + l (16 bytes: rows start on 128-byte lines and hold whole
+// chunks of capacity), its row found by UC lockstep binary searches over the group's chunk
+// prefix; each 256-slot register is then transposed through LDS into slot order, so
+// instruction t of it takes slots 64t .. 64t + 63 in lane order, the order that keeps every
+// column's adds in ascending row order. The decode is branch-free except for the rare P runs
+// of 3+ users and degree classes outside the LDS table.
+template <int UC>
+__device__ __forceinline__ void accumulate_group(double *acc, const RowIndex *ix, int total,
+                                                 const uint32_t *__restrict__ ent,
+                                                 const double *s_beta, const double *s_inv,
+                                                 const double *__restrict__ g_inv,
+                                                 uint32_t *tr) {
   const int lane = lane_id();
-  const int64_t *s_base = reinterpret_cast<const int64_t *>(idx);
-  const int *s_incl = reinterpret_cast<const int *>(idx + kResRows * 8);
-  for (int e0 = 0; e0 < total; e0 += 64 * UF) {
-    // r[q] = number of rows whose inclusive end is <= e[q] (the row holding entry e[q]):
-    // the UF binary searches advance in lockstep (independent LDS reads per step, no
-    // branch), then the UF entry loads issue back to back. Lanes past the end re-read
-    // the last entry and skip the add.
-    int e[UF], r[UF];
+  for (int cb = 0; cb < total; cb += 64 * UC) {
+    int rr[UC], cc[UC];
 #pragma unroll
-    for (int q = 0; q < UF; ++q) {
-      const int x = e0 + q * 64 + lane;
-      e[q] = x < total ? x : total - 1;
-      r[q] = 0;
+    for (int q = 0; q < UC; ++q) {
+      const int c = cb + q * 64 + lane;
+      cc[q] = c < total ? c : total - 1;
+      rr[q] = 0;
     }
 #pragma unroll
     for (int st = 64; st > 0; st >>= 1)
 #pragma unroll
-      for (int q = 0; q < UF; ++q) r[q] += s_incl[r[q] + st - 1] <= e[q] ? st : 0;
-    WEnt w[UF];
+      for (int q = 0; q < UC; ++q) rr[q] += ix->cincl[rr[q] + st - 1] <= cc[q] ? st : 0;
+    uint4 w[UC];
 #pragma unroll
-    for (int q = 0; q < UF; ++q) w[q] = wt_ent[s_base[r[q]] + e[q]];
+    for (int q = 0; q < UC; ++q)
+      w[q] = *reinterpret_cast<const uint4 *>(ent + ix->base[rr[q]] +
+                                              4 * (cc[q] - ix->cexcl[rr[q]]));
+    // the first two slots after the block (a V value or a P run that straddles it)
+    const int cn = cb + 64 * UC;
+    uint32_t pk0 = 0, pk1 = 0;
+    if (cn < total) {  // wave-uniform
+      int rp = 0;
 #pragma unroll
-    for (int q = 0; q < UF; ++q)
-      if (e0 + q * 64 + lane < total)
-        __hip_atomic_fetch_add(&acc[w[q].col - item_begin],
-                               __hiloint2double((int)w[q].hi, (int)w[q].lo), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
-// acc[j - item_begin] += W[i][j] for every item i of user u (ascending), acc = the wave's
-// LDS tile accumulator (zeroed by the caller), idx = its kResIdxBytes row index.
-template <int UF>
-__device__ __forceinline__ void accumulate_user_tile(double *acc, char *idx,
-                                                     const int64_t *__restrict__ user_rowptr,
-                                                     const int32_t *__restrict__ user_items,
-                                                     int64_t u,
-                                                     const uint64_t *__restrict__ wt_meta,
-                                                     const WEnt *__restrict__ wt_ent,
-                                                     int32_t item_begin) {
-  const int lane = lane_id();
-  const int64_t pb = user_rowptr[u], pe = user_rowptr[u + 1];
-  for (int64_t p0 = pb; p0 < pe; p0 += kResRows) {
-    uint64_t m0 = 0, m1 = 0;
-    {
-      const int32_t i0 = p0 + lane < pe ? user_items[p0 + lane] : -1;
-      const int32_t i1 = p0 + 64 + lane < pe ? user_items[p0 + 64 + lane] : -1;
-      if (i0 >= 0) m0 = wt_meta[i0];
-      if (i1 >= 0) m1 = wt_meta[i1];
+      for (int st = 64; st > 0; st >>= 1) rp += ix->cincl[rp + st - 1] <= cn ? st : 0;
+      const uint32_t *p = ent + ix->base[rp] + 4 * (cn - ix->cexcl[rp]);
+      pk0 = p[0];
+      pk1 = p[1];
     }
-    const int total = write_row_index(idx, m0, m1);
-    accumulate_group<UF>(acc, idx, total, wt_ent, item_begin);
-  }
-  wave_sync();
-}
-
-// F[u][j - j0] = sum over items(u) ascending of W[i][j]; the tile's accumulator in LDS (tile
-// doubles per wave) plus two 128-row indexes (LDS, 1.5 KiB each). Rows are taken 128 at a
-// time: their metadata is fetched in one round trip (two loads per lane), then their entries
-// are flattened: lane l takes entries e = e0 + q*64 + l of the concatenated rows (its row
-// found by a binary search over the rows' inclusive length prefix in LDS), so each load
-// instruction moves 64 useful 12-byte entries whatever the row lengths, UF of them in flight
-// per lane. Entries go in with ds_add_f64; entries of one instruction that hit the same
-// column come from rows in lane order, and rows are flattened in ascending order, so each
-// column still receives its rows' values in ascending row order (the order of
-// lg_spread_resource_f64).
-//
-// Persistent waves, software-pipelined over the users u, u+G, u+2G, ... of a wave (G = waves
-// in the grid): a user's chain is row pointers -> item ids -> row metadata -> entries, four
-// dependent memory round trips. While user u's entries are in flight the wave also has in
-// flight the metadata of u+G, the item ids of u+2G and the row pointers of u+3G, so each user
-// costs about one round trip (the first group of 128 items; longer rows add their groups
-// unpipelined).
-template <int UF, bool NT>
-__global__ __launch_bounds__(128) void k_tile_resource(
-    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
-    int32_t item_begin, int32_t tile, double *__restrict__ F, int64_t ldf) {
-  extern __shared__ double lds[];
-  const int wave = threadIdx.x / 64;
-  const int wpb = blockDim.x / 64;
-  const int lane = lane_id();
-  const int64_t G = (int64_t)gridDim.x * wpb;
-  int64_t u = (int64_t)blockIdx.x * wpb + wave;
-  if (u >= n_users) return;
-  double *acc = lds + (int64_t)wave * (tile + 2 * kResIdxBytes / 8);
-  char *idx0 = reinterpret_cast<char *>(acc + tile);
-  char *idx1 = idx0 + kResIdxBytes;
-  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
-
-  auto rows = [&](int64_t v, int64_t &b, int64_t &e) __attribute__((always_inline)) {
-    b = e = 0;
-    if (v < n_users) {
-      b = user_rowptr[v];
-      e = user_rowptr[v + 1];
+#pragma unroll
+    for (int q = 0; q < UC; ++q) {
+      wave_sync();  // the previous register's readers of tr are done
+      reinterpret_cast<uint4 *>(tr)[lane] = w[q];
+      wave_sync();
+      const uint32_t nx0 = q + 1 < UC ? __builtin_amdgcn_readlane(w[(q + 1 < UC) ? q + 1 : q].x, 0) : pk0;
+      const uint32_t nx1 = q + 1 < UC ? __builtin_amdgcn_readlane(w[(q + 1 < UC) ? q + 1 : q].y, 0) : pk1;
+      // the register's 4 slot-ordered instructions t: every LDS read of the 4 is issued
+      // before any add (the reads then overlap instead of waiting one by one)
+      uint32_t X[4], N1[4], N2[4];
+      int R[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int m = 64 * t + lane;  // slot of this 256-slot register, in order
+        X[t] = tr[m];
+        N1[t] = tr[m + 1 < 256 ? m + 1 : 255];
+        N2[t] = tr[m + 2 < 256 ? m + 2 : 255];
+        R[t] = __shfl(rr[q], m >> 2);
+      }
+      N1[3] = lane == 63 ? nx0 : N1[3];
+      N2[3] = lane == 63 ? nx1 : (lane == 62 ? nx0 : N2[3]);
+      int CX[4], LW[4];
+      double AL[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        CX[t] = ix->cexcl[R[t]];
+        LW[t] = ix->len[R[t]];
+        AL[t] = ix->alpha[R[t]];
+      }
+      bool HEAD[4], ISV[4];
+      int COL[4], SROW[4];
+      uint32_t CI[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int m = 64 * t + lane;
+        const int cabs = cb + q * 64 + (m >> 2);
+        SROW[t] = 4 * (cabs - CX[t]) + (m & 3);  // slot within its row
+        ISV[t] = LW[t] < 0;
+        const bool valid = cabs < total && SROW[t] < (LW[t] & 0x7fffffff);
+        HEAD[t] = valid && (ISV[t] ? (SROW[t] % 3) == 0 : !(X[t] & kIsCont));
+        COL[t] = HEAD[t] ? (int)(X[t] & 0xffffu) : 0;
+        CI[t] = ISV[t] ? 0u : ((X[t] >> 16) & kClsMask);
+      }
+      double NUM[4], BE[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        NUM[t] = s_inv[CI[t] < (uint32_t)kInvTab ? CI[t] : 0u];
+        BE[t] = s_beta[COL[t]];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool far = HEAD[t] && !ISV[t] && CI[t] >= (uint32_t)kInvTab;
+        if (__ballot(far))
+          if (far) NUM[t] = g_inv[CI[t]];
+        if (ISV[t]) NUM[t] = __hiloint2double((int)N2[t], (int)N1[t]);  // general_W[i][j]
+        const bool run = HEAD[t] && !ISV[t] && (X[t] & kHasNext);
+        if (__ballot(run)) {  // more users behind this (i, j), ascending v
+          if (run) {
+            NUM[t] += inv_of(N1[t], s_inv, g_inv);
+            if (N1[t] & kHasNext) {
+              NUM[t] += inv_of(N2[t], s_inv, g_inv);
+              if (N2[t] & kHasNext) {  // runs of 4+ (rare): the rest from memory
+                const uint32_t *p = ent + ix->base[R[t]] + SROW[t] + 3;
+                uint32_t y;
+                do {
+                  y = *p++;
+                  NUM[t] += inv_of(y, s_inv, g_inv);
+                } while (y & kHasNext);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        double den = AL[t] * BE[t];
+        if (den == 0.0) den = 1.0;
+        NUM[t] = NUM[t] / den;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (HEAD[t])
+          __hip_atomic_fetch_add(&acc[COL[t]], NUM[t], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-  };
-  auto items = [&](int64_t b, int64_t e, int32_t &i0, int32_t &i1) __attribute__((always_inline)) {
-    i0 = b + lane < e ? user_items[b + lane] : -1;
-    i1 = b + 64 + lane < e ? user_items[b + 64 + lane] : -1;
-  };
-  auto meta = [&](int32_t i0, int32_t i1, uint64_t &m0, uint64_t &m1) __attribute__((always_inline)) {
-    m0 = i0 >= 0 ? wt_meta[i0] : 0;
-    m1 = i1 >= 0 ? wt_meta[i1] : 0;
-  };
-
-  // prologue: user u indexed; u+G's item ids and u+2G's row pointers loaded
-  int64_t b0, e0, b1, e1, b2, e2;
-  rows(u, b0, e0);
-  rows(u + G, b1, e1);
-  rows(u + 2 * G, b2, e2);
-  int32_t ia, ib, ja, jb;
-  items(b0, e0, ia, ib);
-  items(b1, e1, ja, jb);
-  uint64_t ma, mb;
-  meta(ia, ib, ma, mb);
-  char *cur = idx0, *nxt = idx1;
-  int total = write_row_index(cur, ma, mb);
-  for (;;) {
-    int32_t ka, kb;
-    items(b2, e2, ka, kb);           // u+2G
-    uint64_t na, nb;
-    meta(ja, jb, na, nb);            // u+G
-    int64_t b3, e3;
-    rows(u + 3 * G, b3, e3);         // u+3G
-    accumulate_group<UF>(acc, cur, total, wt_ent, item_begin);
-    for (int64_t p0 = b0 + kResRows; p0 < e0; p0 += kResRows) {  // rows beyond 128 items
-      int32_t xa, xb;
-      items(p0, e0, xa, xb);
-      uint64_t ya, yb;
-      meta(xa, xb, ya, yb);
-      const int t2 = write_row_index(cur, ya, yb);
-      accumulate_group<UF>(acc, cur, t2, wt_ent, item_begin);
-    }
-    wave_sync();
-    const bool more = u + G < n_users;
-    if (more) total = write_row_index(nxt, na, nb);
-    double *row = F + u * ldf;
-    for (int j = lane; j < tile; j += 64) {
-      if constexpr (NT) __builtin_nontemporal_store(acc[j], row + j);
-      else row[j] = acc[j];
-      acc[j] = 0.0;
-    }
-    wave_sync();  // zeroes land before the next user's adds
-    if (!more) break;
-    u += G;
-    char *t = cur;
-    cur = nxt;
-    nxt = t;
-    b0 = b1; e0 = e1;
-    b1 = b2; e1 = e2;
-    b2 = b3; e2 = e3;
-    ja = ka; jb = kb;
   }
 }
 
@@ -831,7 +834,7 @@ template <int D>
 __device__ __forceinline__ float chain_score(const float *us, const float *__restrict__ it) {
   constexpr int Q = D / 4;
   float a = 0.f;
-#pragma unroll
+#pragma unroll 1
   for (int s0 = 0; s0 < Q; s0 += 4) {
     float4 q[4];
 #pragma unroll
@@ -847,127 +850,277 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
   return a;
 }
 
-// Per-wave LDS of the fused kernel: the tile accumulator, the row index of
-// accumulate_user_tile, the candidate list (CAP values + ids) and the user's embedding.
-__host__ __device__ constexpr size_t fused_wave_bytes(int tile, int M, int D) {
-  return (size_t)tile * 8 + kResIdxBytes + (size_t)64 * M * 12 + (size_t)D * 4;
+// ------------------------------------------------------------ the tile walk kernel
+// One launch per tile. Persistent waves (NW per workgroup, one workgroup per CU; each wave
+// takes users u, u + G, u + 2G, ... with G = all waves): a user's chain is row pointers ->
+// item ids -> RowMeta -> slots, so while user u's slots are in flight the wave already has
+// the RowMeta of u+G, the item ids of u+2G and the row pointers of u+3G in flight (and, for
+// the top-K mode, u's list, score bounds, embedding and exclusion window).
+//
+// MODE_F:    F[u][j - item_begin] = the accumulator (lg_spread_tile_resource_f64).
+// MODE_TOPK: the tile's columns of (G *) F merge into the running per-user top-K lists
+//            (lg_spread_tile_resource_topk_f64); F never leaves LDS. With a G factor, a
+//            column's score can only beat the list's K-th value tau if gb * F > tau, gb =
+//            the (user, 64-column chunk) upper bound of the fp32 score chain from
+//            lg_score_chunk_bound (bf16 MFMA + a rigorous rounding margin); only those
+//            columns get the exact chain score. Ids grow along the walk, so "beats" is
+//            v > tau (a tie loses to the older, smaller id).
+constexpr int MODE_F = 0, MODE_TOPK = 1;
+
+struct WalkArgs {
+  const int64_t *user_rowptr;
+  const int32_t *user_items;
+  int64_t n_users;
+  const RowMeta *wt_meta;
+  const uint32_t *wt_ent;
+  int32_t item_begin, tile, width;
+  const double *beta;   // all items
+  const double *g_inv;  // fl(1/k) per degree class
+  // MODE_F
+  double *F;
+  int64_t ldf;
+  // MODE_TOPK
+  const float *eu, *ei;       // rows' user embeddings / all item embeddings (or NULL)
+  const float *gb;            // [n_users][nch] score bounds (with eu)
+  int32_t nch;
+  const int64_t *ex_rowptr;   // exclusions (dropped), with a per-row cursor
+  const int32_t *ex_col;
+  int64_t *ex_cur;
+  int k, first;
+  double *io_val;
+  int64_t *io_idx;
+};
+
+template <int MODE, int D, int M>
+__host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
+  return ((size_t)tile * 8 + sizeof(RowIndex) + 1024 +
+          (MODE == MODE_TOPK ? (size_t)64 * M * 12 + (size_t)(D > 0 ? D : 4) * 4 +
+                                   (D > 0 ? (size_t)128 * 12 : 0)
+                             : 0) + 15) &
+         ~(size_t)15;
+}
+__host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
+  return (size_t)tile * 8 + (size_t)kInvTab * 8;
 }
 
-// Fused resource + top-K for one tile (lg_spread_tile_resource_topk_f64): one wave per user.
-// The user's F columns [item_begin, item_begin + width) are accumulated in LDS exactly as
-// k_tile_resource does, the user's excluded items in the tile are marked (-1: F >= 0
-// otherwise), and the columns merge straight into the running list: a column can only enter
-// if (G *) F beats the current K-th value tau. With a G factor, |G| <= ||u|| ||i|| (1 + 1e-4)
-// bounds the fp32 chain (its rounding is < 64 * 2^-24 relative), so once tau > 0 a column
-// with F * bound <= tau is skipped without computing G; the rest get the exact chain score.
-// Ids grow along the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
-template <int UF, int D, int M>
-__global__ __launch_bounds__(128) void k_tile_resource_topk(
-    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_users, const uint64_t *__restrict__ wt_meta, const WEnt *__restrict__ wt_ent,
-    int32_t item_begin, int32_t tile, int32_t width, const float *__restrict__ eu,
-    const float *__restrict__ ei, const double *__restrict__ item_norm,
-    const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col,
-    int64_t *__restrict__ ex_cur, int k, int first, double *__restrict__ io_val,
-    int64_t *__restrict__ io_idx) {
+template <int MODE, int UF, int D, int M>
+__global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   constexpr int CAP = 64 * M;
   extern __shared__ double lds[];
-  const int wave = threadIdx.x / 64;
-  const int wpb = blockDim.x / 64;
+  const int nw = blockDim.x / 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   const int lane = lane_id();
-  const int64_t u = (int64_t)blockIdx.x * wpb + wave;
-  if (u >= n_users) return;
-  char *mine = reinterpret_cast<char *>(lds) + (size_t)wave * fused_wave_bytes(tile, M, D);
+  const int tile = a.tile;
+  double *s_beta = lds;
+  double *s_inv = s_beta + tile;
+  char *mine = reinterpret_cast<char *>(s_inv + kInvTab) +
+               (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
-  char *idx = mine + (size_t)tile * 8;
-  double *cs = reinterpret_cast<double *>(idx + kResIdxBytes);
+  RowIndex *ix = reinterpret_cast<RowIndex *>(acc + tile);
+  uint32_t *tr = reinterpret_cast<uint32_t *>(ix + 1);  // 256-slot transpose scratch
+  double *cs = reinterpret_cast<double *>(tr + 256);
   int *ci = reinterpret_cast<int *>(cs + CAP);
   float *us = reinterpret_cast<float *>(ci + CAP);
+  double *pf = reinterpret_cast<double *>(us + (D > 0 ? D : 4));  // candidate queue (D > 0)
+  int *pj = reinterpret_cast<int *>(pf + 128);
+  (void)cs; (void)ci; (void)us; (void)pf; (void)pj;
 
-  // running list (sorted, valid entries first)
-  int cnt = 0;
-  double tau = neg_inf<double>();
-  int tau_id = kPadId;
-  if (!first) {
-    for (int e0 = 0; e0 < k; e0 += 64) {
-      const int e = e0 + lane;
-      const int64_t id = e < k ? io_idx[u * k + e] : -1;
-      if (id >= 0) {
-        cs[e] = io_val[u * k + e];
-        ci[e] = (int)id;
-      }
-      cnt += __popcll(__ballot(id >= 0));
-    }
-  }
-  double ubound = 0.0;
-  if constexpr (D > 0) {
-    double ss = 0.0;
-    for (int d = lane; d < D; d += 64) {
-      const float x = eu[u * D + d];
-      us[d] = x;
-      ss += (double)x * (double)x;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    ubound = sqrt(ss) * (1.0 + 1e-4);
-  }
+  for (int j = threadIdx.x; j < tile; j += blockDim.x)
+    s_beta[j] = j < a.width ? a.beta[a.item_begin + j] : 0.0;
+  for (int c = threadIdx.x; c < kInvTab; c += blockDim.x) s_inv[c] = a.g_inv[c];
   for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
-  // (accumulate_user_tile's first barrier orders the list / embedding / zero stores)
-  accumulate_user_tile<UF>(acc, idx, user_rowptr, user_items, u, wt_meta, wt_ent, item_begin);
-  if (cnt == k) {
-    tau = cs[k - 1];
-    tau_id = ci[k - 1];
-  }
-  const int lim = item_begin + width;
-  if (ex_rowptr) {
-    // excluded items of the tile: the next run of the user's sorted exclusion row
-    int64_t pos = ex_cur[u];
-    const int64_t hi = ex_rowptr[u + 1];
-    while (pos < hi) {
-      const int64_t e = pos + lane;
-      const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
-      const bool in = x < lim;
-      if (in && x >= item_begin) acc[x - item_begin] = -1.0;
-      const int nin = __popcll(__ballot(in));
-      pos += nin;
-      if (nin < 64) break;
+  __syncthreads();
+
+  const int64_t G = (int64_t)gridDim.x * nw;
+  int64_t u = (int64_t)blockIdx.x * nw + wave;
+  const int64_t n_users = a.n_users;
+  if (u >= n_users) return;
+
+  auto rows = [&](int64_t v, int64_t &b, int64_t &e) __attribute__((always_inline)) {
+    b = e = 0;
+    if (v < n_users) {
+      b = a.user_rowptr[v];
+      e = a.user_rowptr[v + 1];
     }
-    if (lane == 0) ex_cur[u] = pos;
+  };
+  auto items = [&](int64_t b, int64_t e, int32_t &i0, int32_t &i1) __attribute__((always_inline)) {
+    i0 = b + lane < e ? a.user_items[b + lane] : -1;
+    i1 = b + 64 + lane < e ? a.user_items[b + 64 + lane] : -1;
+  };
+  auto meta = [&](int32_t i0, int32_t i1, RowMeta &m0, RowMeta &m1) __attribute__((always_inline)) {
+    m0 = i0 >= 0 ? a.wt_meta[i0] : RowMeta{0, 0.0};
+    m1 = i1 >= 0 ? a.wt_meta[i1] : RowMeta{0, 0.0};
+  };
+
+  int64_t b0, e0, b1, e1, b2, e2;
+  rows(u, b0, e0);
+  rows(u + G, b1, e1);
+  rows(u + 2 * G, b2, e2);
+  int32_t ia, ib, ja, jb;
+  items(b0, e0, ia, ib);
+  items(b1, e1, ja, jb);
+  RowMeta ma, mb;
+  meta(ia, ib, ma, mb);
+  int64_t xc_next = 0;  // exclusion cursor of the next user (MODE_TOPK)
+  if constexpr (MODE == MODE_TOPK)
+    if (a.ex_rowptr) xc_next = a.ex_cur[u];
+  int total = write_row_index(ix, ma, mb);
+  for (;;) {
+    int32_t ka, kb;
+    items(b2, e2, ka, kb);           // u+2G
+    RowMeta na, nb;
+    meta(ja, jb, na, nb);            // u+G
+    int64_t b3, e3;
+    rows(u + 3 * G, b3, e3);         // u+3G
+    // ---- this user's top-K inputs, in flight beside its slots
+    const int k = a.k;
+    int64_t lid0 = -1, lid1 = -1;
+    double lv0 = 0.0, lv1 = 0.0;
+    float gbv = 0.f, uev0 = 0.f, uev1 = 0.f;
+    int64_t xpos = 0, xhi = 0, xc_after = 0;
+    int32_t xw = 0x7fffffff;
+    if constexpr (MODE == MODE_TOPK) {
+      if (!a.first) {
+        if (lane < k) { lid0 = a.io_idx[u * k + lane]; lv0 = a.io_val[u * k + lane]; }
+        if (64 + lane < k) { lid1 = a.io_idx[u * k + 64 + lane]; lv1 = a.io_val[u * k + 64 + lane]; }
+      }
+      if constexpr (D > 0) {
+        if (lane < a.nch) gbv = a.gb[u * a.nch + lane];
+        if (lane < D) uev0 = a.eu[u * D + lane];
+        if (D > 64 && 64 + lane < D) uev1 = a.eu[u * D + 64 + lane];
+      }
+      if (a.ex_rowptr) {
+        xpos = xc_next;
+        xhi = a.ex_rowptr[u + 1];
+        if (u + G < n_users) xc_after = a.ex_cur[u + G];
+        if (xpos + lane < xhi) xw = a.ex_col[xpos + lane];
+      }
+    }
+    accumulate_group<UF>(acc, ix, total, a.wt_ent, s_beta, s_inv, a.g_inv, tr);
+    for (int64_t p0 = b0 + kResRows; p0 < e0; p0 += kResRows) {  // rows beyond 128 items
+      int32_t xa, xb;
+      items(p0, e0, xa, xb);
+      RowMeta ya, yb;
+      meta(xa, xb, ya, yb);
+      const int t2 = write_row_index(ix, ya, yb);
+      accumulate_group<UF>(acc, ix, t2, a.wt_ent, s_beta, s_inv, a.g_inv, tr);
+    }
     wave_sync();
-  }
-  for (int c0 = 0; c0 < width; c0 += 64) {
-    const int j = c0 + lane;
-    const double f = j < width ? acc[j] : -1.0;
-    bool cand = f >= 0.0;
-    double v = f;
-    if constexpr (D > 0) {
-      if (cand && tau > 0.0) cand = f * (ubound * item_norm[item_begin + j]) > tau;
-      if (__ballot(cand)) {
-        if (cand) v = (double)chain_score<D>(us, ei + (int64_t)(item_begin + j) * D) * f;
-        cand = cand && v > tau;
+    if constexpr (MODE == MODE_F) {
+      double *row = a.F + u * a.ldf;
+      for (int j = lane; j < tile; j += 64) {
+        __builtin_nontemporal_store(acc[j], row + j);
+        acc[j] = 0.0;
       }
     } else {
-      cand = cand && v > tau;
-    }
-    const uint64_t bal = __ballot(cand);
-    if (bal) {
-      const int p = cnt + __popcll(bal & lanemask_lt());
-      if (cand) {
-        cs[p] = v;
-        ci[p] = item_begin + j;
+      // running list -> LDS (valid entries form a sorted prefix)
+      int cnt = __popcll(__ballot(lid0 >= 0)) + __popcll(__ballot(lid1 >= 0));
+      if (lid0 >= 0) { cs[lane] = lv0; ci[lane] = (int)lid0; }
+      if (lid1 >= 0) { cs[64 + lane] = lv1; ci[64 + lane] = (int)lid1; }
+      if constexpr (D > 0) {
+        if (lane < D) us[lane] = uev0;
+        if (D > 64 && 64 + lane < D) us[64 + lane] = uev1;
       }
-      cnt += __popcll(bal);
-      if (cnt > CAP - 64) {
+      // excluded items of this tile (the next run of the user's sorted exclusion row): -1
+      const int32_t lim = a.item_begin + a.width;
+      if (a.ex_rowptr) {
+        for (;;) {
+          const bool in = xw < lim;
+          if (in && xw >= a.item_begin) acc[xw - a.item_begin] = -1.0;
+          const int nin = __popcll(__ballot(in));
+          xpos += nin;
+          if (nin < 64) break;
+          xw = xpos + lane < xhi ? a.ex_col[xpos + lane] : 0x7fffffff;  // > 64 in one tile
+        }
+        if (lane == 0) a.ex_cur[u] = xpos;
+      }
+      wave_sync();
+      double tau = neg_inf<double>();
+      int tau_id = kPadId;
+      if (cnt == k) { tau = cs[k - 1]; tau_id = ci[k - 1]; }
+      bool dirty = a.first != 0;
+      // insert the lanes' (v, item) with cand set; compact when the list could overflow
+      auto insert = [&](bool cand, double v, int item) __attribute__((always_inline)) {
+        const uint64_t bal = __ballot(cand);
+        if (!bal) return;
+        dirty = true;
+        const int p = cnt + __popcll(bal & lanemask_lt());
+        if (cand) {
+          cs[p] = v;
+          ci[p] = item;
+        }
+        cnt += __popcll(bal);
+        if (cnt > CAP - 64) {
+          wave_sync();
+          cnt = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
+        }
+      };
+      if constexpr (D > 0) {
+        // columns whose bound gb * F beats tau are queued (pj/pf, ascending), and scored
+        // 64 at a time, one lane each: one round of item-row loads per 64 candidates
+        int np = 0;
+        auto flush = [&](int m) __attribute__((always_inline)) {
+          wave_sync();
+          bool cand = lane < m;
+          double v = 0.0;
+          int item = 0;
+          if (cand) {
+            item = a.item_begin + pj[lane];
+            v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * pf[lane];
+            cand = v > tau;
+          }
+          wave_sync();
+          if (np > 64) {  // keep the queue's tail
+            if (lane < np - 64) { pj[lane] = pj[64 + lane]; pf[lane] = pf[64 + lane]; }
+          }
+          np = np > 64 ? np - 64 : 0;
+          insert(cand, v, item);
+        };
+        for (int c0 = 0; c0 < a.width; c0 += 64) {
+          const int j = c0 + lane;
+          const double f = j < a.width ? acc[j] : -1.0;
+          if (j < tile) acc[j] = 0.0;
+          const float gbc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gbv), c0 >> 6));
+          const bool cand = f >= 0.0 && (double)gbc * f > tau;
+          const uint64_t bal = __ballot(cand);
+          if (bal) {
+            const int p = np + __popcll(bal & lanemask_lt());
+            if (cand) {
+              pj[p] = j;
+              pf[p] = f;
+            }
+            np += __popcll(bal);
+            if (np >= 64) flush(64);
+          }
+        }
+        while (np > 0) flush(np < 64 ? np : 64);
+      } else {
+        for (int c0 = 0; c0 < a.width; c0 += 64) {
+          const int j = c0 + lane;
+          const double f = j < a.width ? acc[j] : -1.0;
+          if (j < tile) acc[j] = 0.0;
+          insert(f >= 0.0 && f > tau, f, a.item_begin + j);
+        }
+      }
+      if (dirty) {
         wave_sync();
-        cnt = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
+        const int nc = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
+        for (int e = lane; e < k; e += 64) {
+          a.io_val[u * k + e] = e < nc ? cs[e] : neg_inf<double>();
+          a.io_idx[u * k + e] = e < nc ? ci[e] : -1;
+        }
       }
+      wave_sync();
+      xc_next = xc_after;
     }
-  }
-  wave_sync();
-  const int nc = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
-  for (int e = lane; e < k; e += 64) {
-    io_val[u * k + e] = e < nc ? cs[e] : neg_inf<double>();
-    io_idx[u * k + e] = e < nc ? ci[e] : -1;
+    const bool more = u + G < n_users;
+    if (!more) break;
+    total = write_row_index(ix, na, nb);
+    u += G;
+    b0 = b1; e0 = e1;
+    b1 = b2; e1 = e2;
+    b2 = b3; e2 = e3;
+    ja = ka; jb = kb;
   }
 }
 
@@ -1162,14 +1315,15 @@ extern "C" size_t lg_spread_tile_weight_ws_bytes(int64_t n_items) {
 }
 
 extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                                         const int32_t *user_items, const double *inv_deg,
-                                         int64_t n_items, const int64_t *cur,
-                                         const uint16_t *count, const double *alpha,
-                                         const double *beta, int32_t item_begin, int32_t tile,
-                                         const int64_t *wt_ptr, void *wt_ent, uint64_t *wt_meta,
+                                         const int32_t *user_items, const uint16_t *user_cls,
+                                         const double *inv_deg, int64_t n_items,
+                                         const int64_t *cur, const uint16_t *count,
+                                         const double *alpha, const double *beta,
+                                         int32_t item_begin, int32_t tile, const int64_t *bound,
+                                         const int64_t *wt_ptr, void *wt_ent, void *wt_meta,
                                          void *ws, size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && inv_deg && cur && count && alpha && beta && wt_ptr && wt_meta &&
-                 n_items >= 0,
+  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && count && alpha && beta && bound &&
+                 wt_ptr && wt_ent && wt_meta && n_items >= 0,
              "lg_spread_tile_weight_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && item_begin >= 0,
              "lg_spread_tile_weight_f64: tile %d not in [1, 8192]", tile);
@@ -1187,31 +1341,18 @@ extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32
     return LG_ERR_HIP;
   }
   const unsigned rb = (unsigned)((n_items + 3) / 4);
-  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_items, inv_deg,
-                                               n_items, cur, count, alpha, beta, wt_ptr,
-                                               (WEnt *)wt_ent, wt_meta);
+  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_items, user_cls,
+                                               n_items, cur, count, alpha, item_begin, bound,
+                                               wt_ptr, (uint32_t *)wt_ent, (RowMeta *)wt_meta);
   k_hub_list<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
-      wt_ptr, n_items, (unsigned long long *)n_hub, hub_rows);
+      bound, n_items, (unsigned long long *)n_hub, hub_rows);
   k_tile_weight_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
       hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, alpha, beta,
-      item_begin, tile, wt_ptr, (WEnt *)wt_ent, wt_meta);
+      item_begin, tile, wt_ptr, (uint32_t *)wt_ent, (RowMeta *)wt_meta);
   return launch_status("lg_spread_tile_weight_f64");
 }
 
-extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
-                                           const int32_t *user_items, int64_t n_users,
-                                           const uint64_t *wt_meta, const void *wt_ent,
-                                           int32_t item_begin, int32_t tile, double *F,
-                                           int64_t ldf, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && wt_meta && F && n_users >= 0 && ldf >= tile,
-             "lg_spread_tile_resource_f64: bad arguments");
-  LG_REQUIRE(tile >= 1 && tile <= 8192, "lg_spread_tile_resource_f64: tile %d not in [1, 8192]",
-             tile);
-  if (n_users == 0) return LG_OK;
-  // per wave: tile doubles + two row indexes; 2-wave blocks, as many resident per CU as the
-  // LDS holds, and a persistent grid of exactly that many (each wave walks users u + k*G)
-  const size_t per_wave = (size_t)tile * sizeof(double) + 2 * kResIdxBytes;
-  const size_t lds = 2 * per_wave;
+static int n_cus() {
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -1220,32 +1361,56 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
         n_cu <= 0)
       n_cu = 256;
   }
-  // LGCNHS_RES_BLOCKS_PER_CU (A/B knob): resident-block multiple of the persistent grid;
-  // 0 = one wave per user (no persistence)
-  static int mult = -1;
-  if (mult < 0) {
-    const char *e = getenv("LGCNHS_RES_BLOCKS_PER_CU");
-    mult = e ? atoi(e) : 0;
+  return n_cu;
+}
+
+// waves per workgroup: as many as the LDS holds next to the shared tables (<= 8), one
+// workgroup per CU, persistent
+template <int MODE, int UF, int D, int M>
+static int launch_walk(const WalkArgs &a, hipStream_t s) {
+  const size_t per = walk_wave_bytes<MODE, D, M>(a.tile);
+  const size_t shared = walk_shared_bytes(a.tile);
+  const size_t budget = 160 * 1024;
+  int nw = (int)((budget - shared) / per);
+  if (nw > 8) nw = 8;
+  if (nw < 1) {
+    set_error("tile walk: tile %d needs %zu bytes of LDS per wave", a.tile, per + shared);
+    return LG_ERR_ARG;
   }
-  const int64_t per_cu = (int64_t)(160 * 1024 / lds) > 0 ? (int64_t)(160 * 1024 / lds) : 1;
-  const int64_t want = (n_users + 1) / 2;
-  const int64_t cap = mult > 0 ? per_cu * n_cu * mult : want;
+  const int64_t want = (a.n_users + nw - 1) / nw;
+  const int64_t cap = n_cus();
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
-  // F rows are written with non-temporal stores: they are read once, by the next top-K
-  // span, and should not displace W tile lines (1M users, 40 tiles: 4.08-4.14 vs 4.26 s of
-  // resource passes, top-K unchanged; non-temporal F loads in the top-K measured 4 % slower).
-  // LGCNHS_RES_NT=0 (A/B knob) restores plain stores.
-  static int nt = -1;
-  if (nt < 0) {
-    const char *e = getenv("LGCNHS_RES_NT");
-    nt = e ? atoi(e) : 1;
-  }
-  if (nt)
-    k_tile_resource<16, true><<<dim3(blocks), dim3(128), lds, (hipStream_t)stream>>>(
-        user_rowptr, user_items, n_users, wt_meta, (const WEnt *)wt_ent, item_begin, tile, F, ldf);
-  else
-    k_tile_resource<16, false><<<dim3(blocks), dim3(128), lds, (hipStream_t)stream>>>(
-        user_rowptr, user_items, n_users, wt_meta, (const WEnt *)wt_ent, item_begin, tile, F, ldf);
+  const size_t lds = shared + (size_t)nw * per;
+  k_tile_walk<MODE, UF, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
+  return LG_OK;
+}
+
+extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
+                                           const int32_t *user_items, int64_t n_users,
+                                           const void *wt_meta, const void *wt_ent,
+                                           const double *beta, const double *inv_cls,
+                                           int32_t item_begin, int32_t tile, int32_t width,
+                                           double *F, int64_t ldf, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && wt_meta && beta && inv_cls && F && n_users >= 0 && ldf >= tile,
+             "lg_spread_tile_resource_f64: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile,
+             "lg_spread_tile_resource_f64: tile %d / width %d", tile, width);
+  if (n_users == 0) return LG_OK;
+  WalkArgs a{};
+  a.user_rowptr = user_rowptr;
+  a.user_items = user_items;
+  a.n_users = n_users;
+  a.wt_meta = (const RowMeta *)wt_meta;
+  a.wt_ent = (const uint32_t *)wt_ent;
+  a.item_begin = item_begin;
+  a.tile = tile;
+  a.width = width;
+  a.beta = beta;
+  a.g_inv = inv_cls;
+  a.F = F;
+  a.ldf = ldf;
+  const int st = launch_walk<MODE_F, 4, 0, 1>(a, (hipStream_t)stream);
+  if (st != LG_OK) return st;
   return launch_status("lg_spread_tile_resource_f64");
 }
 
@@ -1281,59 +1446,82 @@ extern "C" int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows,
 }
 
 extern "C" size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim) {
+  // one wave's share plus the workgroup's tables (the launch fits as many waves as it can)
   const int M = k <= 64 ? 2 : 4;
-  return 2 * fused_wave_bytes(tile, M, dim);
+  const size_t per = M == 2 ? (dim > 64 ? walk_wave_bytes<MODE_TOPK, 128, 2>(tile)
+                                        : walk_wave_bytes<MODE_TOPK, 64, 2>(tile))
+                            : walk_wave_bytes<MODE_TOPK, 128, 4>(tile);
+  return per + walk_shared_bytes(tile);
 }
 
 template <int D>
-static void launch_fused(int M, const int64_t *user_rowptr, const int32_t *user_items,
-                         int64_t n_users, const uint64_t *wt_meta, const WEnt *wt_ent,
-                         int32_t item_begin, int32_t tile, int32_t width, const float *eu,
-                         const float *ei, const double *item_norm, const int64_t *ex_rowptr,
-                         const int32_t *ex_col, int64_t *ex_cur, int k, int first,
-                         double *io_val, int64_t *io_idx, hipStream_t s) {
-  const unsigned b = (unsigned)((n_users + 1) / 2);
-  const size_t lds = 2 * fused_wave_bytes(tile, M, D);
-  if (M == 2)
-    k_tile_resource_topk<16, D, 2><<<b, 128, lds, s>>>(
-        user_rowptr, user_items, n_users, wt_meta, wt_ent, item_begin, tile, width, eu, ei,
-        item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx);
-  else
-    k_tile_resource_topk<16, D, 4><<<b, 128, lds, s>>>(
-        user_rowptr, user_items, n_users, wt_meta, wt_ent, item_begin, tile, width, eu, ei,
-        item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx);
+static int launch_fused(int M, const WalkArgs &a, hipStream_t s) {
+  // LGCNHS_WALK_UC (A/B knob): 4-slot chunk registers per block (2 or 8; default 4)
+  static int uc = -1;
+  if (uc < 0) {
+    const char *e = getenv("LGCNHS_WALK_UC");
+    uc = e ? atoi(e) : 4;
+  }
+  if (M == 2 && uc == 2) return launch_walk<MODE_TOPK, 2, D, 2>(a, s);
+  if (M == 2 && uc == 8) return launch_walk<MODE_TOPK, 8, D, 2>(a, s);
+  return M == 2 ? launch_walk<MODE_TOPK, 4, D, 2>(a, s) : launch_walk<MODE_TOPK, 4, D, 4>(a, s);
 }
 
 extern "C" int lg_spread_tile_resource_topk_f64(
     const int64_t *user_rowptr, const int32_t *user_items, int64_t n_users,
-    const uint64_t *wt_meta, const void *wt_ent, int32_t item_begin, int32_t tile,
-    int32_t width, const float *eu, const float *ei, int32_t dim, const double *item_norm,
-    const int64_t *ex_rowptr, const int32_t *ex_col, int64_t *ex_cur, int32_t k,
-    int32_t first, double *io_val, int64_t *io_idx, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && wt_meta && io_val && io_idx && n_users >= 0 && item_begin >= 0,
+    const void *wt_meta, const void *wt_ent, const double *beta, const double *inv_cls,
+    int32_t item_begin, int32_t tile, int32_t width, const float *eu, const float *ei,
+    int32_t dim, const float *gb, int32_t n_chunks, const int64_t *ex_rowptr,
+    const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
+    int64_t *io_idx, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && wt_meta && beta && inv_cls && io_val && io_idx && n_users >= 0 &&
+                 item_begin >= 0,
              "lg_spread_tile_resource_topk_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile &&
                  (int64_t)item_begin + width < 0x7fffffff,
              "lg_spread_tile_resource_topk_f64: tile %d / width %d", tile, width);
   LG_REQUIRE(k >= 1 && k <= 128, "lg_spread_tile_resource_topk_f64: k=%d not in [1,128]", k);
-  LG_REQUIRE(!eu == !ei && (!eu || item_norm),
-             "lg_spread_tile_resource_topk_f64: eu, ei and item_norm go together");
+  LG_REQUIRE(!eu == !ei && !eu == !gb,
+             "lg_spread_tile_resource_topk_f64: eu, ei and gb go together");
   LG_REQUIRE(!eu || dim == 32 || dim == 64 || dim == 128,
              "lg_spread_tile_resource_topk_f64: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(!eu || n_chunks == (width + 63) / 64,
+             "lg_spread_tile_resource_topk_f64: n_chunks %d != ceil(width / 64)", n_chunks);
   LG_REQUIRE(!ex_rowptr == !ex_col && !ex_rowptr == !ex_cur,
              "lg_spread_tile_resource_topk_f64: ex_rowptr/ex_col/ex_cur go together");
-  LG_REQUIRE(lg_spread_tile_resource_topk_lds_bytes(tile, k, eu ? dim : 0) <= 160 * 1024,
-             "lg_spread_tile_resource_topk_f64: tile %d needs too much LDS", tile);
   if (n_users == 0) return LG_OK;
+  WalkArgs a{};
+  a.user_rowptr = user_rowptr;
+  a.user_items = user_items;
+  a.n_users = n_users;
+  a.wt_meta = (const RowMeta *)wt_meta;
+  a.wt_ent = (const uint32_t *)wt_ent;
+  a.item_begin = item_begin;
+  a.tile = tile;
+  a.width = width;
+  a.beta = beta;
+  a.g_inv = inv_cls;
+  a.eu = eu;
+  a.ei = ei;
+  a.gb = gb;
+  a.nch = n_chunks;
+  a.ex_rowptr = ex_rowptr;
+  a.ex_col = ex_col;
+  a.ex_cur = ex_cur;
+  a.k = k;
+  a.first = first;
+  a.io_val = io_val;
+  a.io_idx = io_idx;
   hipStream_t s = (hipStream_t)stream;
   const int M = k <= 64 ? 2 : 4;
-  const WEnt *w = (const WEnt *)wt_ent;
+  int st;
   switch (eu ? dim : 0) {
-    case 0: launch_fused<0>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
-    case 32: launch_fused<32>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
-    case 64: launch_fused<64>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
-    default: launch_fused<128>(M, user_rowptr, user_items, n_users, wt_meta, w, item_begin, tile, width, eu, ei, item_norm, ex_rowptr, ex_col, ex_cur, k, first, io_val, io_idx, s); break;
+    case 0: st = launch_fused<0>(M, a, s); break;
+    case 32: st = launch_fused<32>(M, a, s); break;
+    case 64: st = launch_fused<64>(M, a, s); break;
+    default: st = launch_fused<128>(M, a, s); break;
   }
+  if (st != LG_OK) return st;
   return launch_status("lg_spread_tile_resource_topk_f64");
 }
 

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -343,9 +344,39 @@ def hybrid_factors(k_item: torch.Tensor, lam: float):
     return alpha, beta
 
 
+SORT_MAX = 256     # pairs per row of the in-wave sort: longer rows are hub (V) rows
+INV_TAB = 512      # degree classes cached in LDS by the walk (csrc/spread_tiled.hip)
+MAX_CLASSES = 0x3FFF
+
+
+def degree_classes(deg: torch.Tensor):
+    """(class of each row's degree as uint16, fp64 fl(1/k) per class): the P-row slot code
+    of csrc/spread_tiled.hip. Classes are ordered by how many rows have the degree, so the
+    common ones fall in the walk's LDS table. Rows of degree 0 get class 0 (never used)."""
+    dev = deg.device
+    pos = deg[deg > 0]
+    if pos.numel() == 0:
+        return (torch.zeros(deg.numel(), dtype=torch.int16, device=dev).view(torch.uint16),
+                torch.zeros(INV_TAB, dtype=torch.float64, device=dev))
+    uniq, counts = torch.unique(pos, return_counts=True)
+    if uniq.numel() >= MAX_CLASSES:
+        raise ValueError(f"{uniq.numel()} distinct user degrees: the tile format encodes at "
+                         f"most {MAX_CLASSES - 1} (use the dense spreading path)")
+    order = torch.argsort(counts, descending=True, stable=True)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), device=dev)
+    cls = torch.zeros(deg.numel(), dtype=torch.int32, device=dev)
+    m = deg > 0
+    cls[m] = rank[torch.searchsorted(uniq, deg[m])].to(torch.int32)
+    inv = torch.zeros(max(INV_TAB, uniq.numel()), dtype=torch.float64, device=dev)
+    inv[:uniq.numel()] = 1.0 / uniq[order].to(torch.float64)
+    return cls.to(torch.int16).view(torch.uint16), inv
+
+
 class TileWeights:
     """W = HybridS(general_W) restricted to one item tile, row-major over all items
-    (lg_spread_tile_* of include/lgcnhs.h). ``advance()`` moves to the next tile; the
+    (lg_spread_tile_* of include/lgcnhs.h; P rows = the (user, item) pairs as 4-byte slots,
+    V rows = merged fp64 values of hub items). ``advance()`` moves to the next tile; the
     buffers are reused and grown on demand."""
 
     def __init__(self, A: Interactions, lam: float, tile: int):
@@ -363,37 +394,70 @@ class TileWeights:
         N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,
                                           N.ptr(self.inv_deg), N.stream_handle(dev)),
                 "lg_inv_degree_f64")
+        self.user_cls, self.inv_cls = degree_classes(A.by_user.degrees())
         self.bound = torch.empty(I, dtype=torch.int64, device=dev)
         self.ptr = torch.zeros(I + 1, dtype=torch.int64, device=dev)
-        self.meta = torch.empty(I, dtype=torch.int64, device=dev)  # ptr | len << 48
+        self.meta = torch.empty((I, 2), dtype=torch.int64, device=dev)  # {ptr|len<<40|V<<63, alpha}
         self.ws = torch.empty(max(1, N.lib().lg_spread_tile_weight_ws_bytes(I)),
                               dtype=torch.uint8, device=dev)
-        self.ent = torch.empty(0, dtype=torch.int32, device=dev)  # 3 int32 per entry
+        self.ent = torch.empty(0, dtype=torch.int32, device=dev)  # 4-byte slots
         self.j0 = None
         self.width = 0
         self._seek_at = None
-        # Row alignment in entries: 32 x 12 B = 384 B = 3 lines, so a row of n entries spans
-        # ceil(12n / 128) lines instead of one more on average at a random start (the
-        # resource pass gathers ~10^12 entries at C5 and is fabric-bound). Capacities stay
-        # > 256 exactly for the hub rows since 256 is a multiple of 32.
+        # Rows start on 128-B lines (32 slots): a P row of n pairs then spans ceil(4n / 128)
+        # lines instead of one more on average at a random start.
         self.align = int(os.environ.get("LGCNHS_W_ALIGN", "32"))
-        if self.align < 1 or self.align & (self.align - 1) or 256 % self.align:
-            raise ValueError(f"LGCNHS_W_ALIGN={self.align}: a power of two dividing 256")
+        if self.align < 1 or self.align & (self.align - 1):
+            raise ValueError(f"LGCNHS_W_ALIGN={self.align}: a power of two")
 
     @property
     def len(self) -> torch.Tensor:
-        """Entries of each W row in the current tile."""
-        return (self.meta >> 48).to(torch.int32)
+        """Slots of each row in the current tile."""
+        return ((self.meta[:, 0] >> 40) & ((1 << 23) - 1)).to(torch.int64)
 
     @property
-    def col(self) -> torch.Tensor:
-        """Item of each entry slot (row i's entries at ptr[i] .. ptr[i] + len[i])."""
-        return self.ent.view(-1, 3)[:, 0]
+    def is_hub(self) -> torch.Tensor:
+        """True for V (merged-value) rows."""
+        return self.meta[:, 0] < 0
 
-    @property
-    def val(self) -> torch.Tensor:
-        """Value of each entry slot (fp64 stored as two int32 words)."""
-        return self.ent.view(-1, 3)[:, 1:].contiguous().view(torch.float64).view(-1)
+    def dense(self) -> torch.Tensor:
+        """The current tile of W as a dense [I, width] fp64 matrix (host, test helper): P
+        runs summed in slot order and divided by alpha_i * beta_j exactly as the walk does,
+        V values as stored."""
+        meta = self.meta.cpu()
+        ptr = (meta[:, 0] & ((1 << 40) - 1)).numpy()
+        ln = ((meta[:, 0] >> 40) & ((1 << 23) - 1)).numpy()
+        hub = (meta[:, 0] < 0).numpy()
+        alpha = meta[:, 1].contiguous().view(torch.float64).numpy()
+        beta = self.beta.cpu().numpy()[self.j0:self.j0 + self.width]
+        inv = self.inv_cls.cpu().numpy()
+        ent = self.ent.cpu().numpy().view(np.uint32)
+        out = np.zeros((self.A.n_items, self.width))
+        for i in np.nonzero(ln)[0]:
+            sl = ent[ptr[i]:ptr[i] + ln[i]]
+            if hub[i]:
+                t = sl.reshape(-1, 3)
+                assert np.all((t[:, 0] >> 16) & 0x3FFF == 0x3FFF)
+                col = (t[:, 0] & 0xFFFF).astype(np.int64)
+                gw = (t[:, 1].astype(np.uint64) | (t[:, 2].astype(np.uint64) << 32)).view(np.float64)
+                assert np.all(np.diff(col) > 0)
+                den = alpha[i] * beta[col]
+                out[i, col] = gw / np.where(den != 0.0, den, 1.0)
+                continue
+            col = (sl & 0xFFFF).astype(np.int64)
+            cls = (sl >> 16) & 0x3FFF
+            cont = (sl >> 31) & 1
+            nxt = (sl >> 30) & 1
+            assert np.all(np.diff(col) >= 0) and np.all(col < self.width)
+            assert np.array_equal(cont[1:], nxt[:-1]) and cont[0] == 0 and nxt[-1] == 0
+            assert np.all((np.diff(col) == 0) == (cont[1:] == 1))
+            s, c0 = 0.0, -1
+            for t in range(sl.size):
+                s = inv[cls[t]] if not cont[t] else s + inv[cls[t]]
+                if not nxt[t]:
+                    den = alpha[i] * beta[col[t]]
+                    out[i, col[t]] = s / (den if den != 0.0 else 1.0)
+        return out
 
     def seek(self, j0: int) -> None:
         """Start the tile walk at item j0 instead of 0 (an item-range shard): the next
@@ -431,32 +495,37 @@ class TileWeights:
         N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
                                        N.ptr(self.count), N.ptr(self.bound), strm),
                 "lg_spread_tile_bound")
-        if self.align > 1:  # row capacities rounded up: every row starts on a 128-B line
-            torch.cumsum(torch.bitwise_and(self.bound + (self.align - 1), -self.align), 0,
-                         out=self.ptr[1:])
-        else:
-            torch.cumsum(self.bound, 0, out=self.ptr[1:])
+        # row capacities in slots: P rows hold their pairs, V (hub) rows one triple per
+        # distinct column
+        cap = torch.where(self.bound <= SORT_MAX, self.bound,
+                          3 * torch.clamp(self.bound, max=self.tile))
+        if self.align > 1:
+            cap = torch.bitwise_and(cap + (self.align - 1), -self.align)
+        torch.cumsum(cap, 0, out=self.ptr[1:])
         total = int(self.ptr[-1])  # host sync: sizes the row storage
-        if 3 * total > self.ent.numel():
-            cap = max(total, int(self.ent.numel() // 3 * 1.25))
-            self.ent = torch.empty(3 * cap, dtype=torch.int32, device=self.dev)
+        if total >= 1 << 40:
+            raise ValueError("tile too large for the 40-bit row pointers")
+        if total > self.ent.numel():
+            n = max(total, int(self.ent.numel() * 1.25))
+            self.ent = torch.empty(n, dtype=torch.int32, device=self.dev)
         N.check(L.lg_spread_tile_weight_f64(
             N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
-            N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count), N.ptr(self.alpha),
-            N.ptr(self.beta), j0, self.tile, N.ptr(self.ptr), N.ptr(self.ent),
-            N.ptr(self.meta), N.ptr(self.ws), self.ws.numel(), strm),
-            "lg_spread_tile_weight_f64")
+            N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count),
+            N.ptr(self.alpha), N.ptr(self.beta), j0, self.tile, N.ptr(self.bound),
+            N.ptr(self.ptr), N.ptr(self.ent), N.ptr(self.meta), N.ptr(self.ws),
+            self.ws.numel(), strm), "lg_spread_tile_weight_f64")
         self.j0, self.width = j0, width
         if getattr(self, "row_uses", None) is not None:
-            self.entries_read += (self.row_uses * (self.meta >> 48)).sum()
+            self.slots_read += (self.row_uses * self.len).sum()
 
     def resource(self, u0: int, u1: int, out: torch.Tensor) -> torch.Tensor:
         """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
         A = self.A
         N.check(N.lib().lg_spread_tile_resource_f64(
             N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), u1 - u0, N.ptr(self.meta),
-            N.ptr(self.ent), self.j0, self.tile, N.ptr(out), out.stride(0),
-            N.stream_handle(self.dev)), "lg_spread_tile_resource_f64")
+            N.ptr(self.ent), N.ptr(self.beta), N.ptr(self.inv_cls), self.j0, self.tile,
+            self.width, N.ptr(out), out.stride(0), N.stream_handle(self.dev)),
+            "lg_spread_tile_resource_f64")
         return out
 
 
@@ -486,20 +555,19 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     never holds general_W, W (I x I) or F (U x I). Bitwise the result of
     spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
 
-    Each tile of W (user-independent) is built once and applied to all the users; the F
-    columns of consecutive tiles are collected in a [users, span] scratch (span = as many
-    whole tiles as ``scratch_bytes`` allows) and merged into the running top-k lists once
-    per span. ``users`` restricts the output to a row range; ``items`` restricts the
+    Each tile of W (user-independent) is built once and walked by every user
+    (lg_spread_tile_resource_topk_f64): the user's F columns are summed in LDS and merged
+    into its running top-k list in the same pass. With a G factor (SpreadLightGCN) the
+    per-(user, 64-column chunk) score bounds of lg_score_chunk_bound (bf16 MFMA) screen the
+    columns, so only those whose bound times F can beat the list's k-th value get the exact
+    fp32 score chain. ``users`` restricts the output to a row range; ``items`` restricts the
     candidates to an item range (the lists of disjoint item ranges merge, with
-    merge_topk_lists, into the full lists: the multi-GPU item shard). fused=True merges each
-    tile's columns into the lists inside the resource kernel
-    (lg_spread_tile_resource_topk_f64): F never leaves LDS and no scratch is used. It is the
-    default without a G factor; with one (SpreadLightGCN), the score of every surviving
-    column must be computed per user from global item rows, which costs more than the F
-    round trip (C5: 14.4 s fused vs 8.1 s with the 16-user MFMA tiles of lg_tile_topk_f64),
-    so the default there is the two-kernel path. ``stats`` (optional dict) receives
-    "w_entries_read": the W entries the resource pass gathers, sum over tiles and users u of
-    sum_{i in items(u)} |row i of W in the tile| (= the path updates of F = A W)."""
+    merge_topk_lists, into the full lists: the multi-GPU item shard). fused=False keeps the
+    two-kernel form (F columns of a span of tiles written to a [users, span] scratch of
+    ``scratch_bytes``, then lg_tile_topk_f64). ``stats`` (optional dict) receives
+    "w_slots_read": the 4-byte W slots the walk gathers, sum over tiles and users u of
+    sum_{i in items(u)} |row i of W in the tile| (= the (i, v, j) paths of F = A W, plus
+    the hub rows' merged triples)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -516,28 +584,26 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     ex = excl.slice_rows(u0, u1) if excl is not None else None
     eu_r = None if eu is None else eu[u0:u1]
     if fused is None:
-        fused = eu is None
+        fused = True
     if stats is not None:
         # users of each item among [u0, u1): the times its W row is gathered per tile
         cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
         tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
-        tw.entries_read = torch.zeros((), dtype=torch.int64, device=dev)
+        tw.slots_read = torch.zeros((), dtype=torch.int64, device=dev)
     if fused:
         _fused_walk(A, tw, u0, u1, i0, i1, k, ex if drop else None, eu_r, ei, vals, idxs)
-        if stats is not None:
-            stats["w_entries_read"] = stats.get("w_entries_read", 0) + int(tw.entries_read)
-        return vals, idxs
-    span = max(tile, scratch_bytes // (n * 8) // tile * tile)
-    span = min(span, -(-(i1 - i0) // tile) * tile)
-    F = torch.empty((n, span), dtype=torch.float64, device=dev)
-    for s0 in range(i0, i1, span):
-        s1 = min(i1, s0 + span)
-        for j0 in range(s0, s1, tile):
-            tw.build(j0, stop=i1)
-            tw.resource(u0, u1, F[:, j0 - s0:])
-        tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
+    else:
+        span = max(tile, scratch_bytes // (n * 8) // tile * tile)
+        span = min(span, -(-(i1 - i0) // tile) * tile)
+        F = torch.empty((n, span), dtype=torch.float64, device=dev)
+        for s0 in range(i0, i1, span):
+            s1 = min(i1, s0 + span)
+            for j0 in range(s0, s1, tile):
+                tw.build(j0, stop=i1)
+                tw.resource(u0, u1, F[:, j0 - s0:])
+            tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
     if stats is not None:
-        stats["w_entries_read"] = stats.get("w_entries_read", 0) + int(tw.entries_read)
+        stats["w_slots_read"] = stats.get("w_slots_read", 0) + int(tw.slots_read)
     return vals, idxs
 
 
@@ -550,32 +616,167 @@ def row_norms(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def bound_operands(x: torch.Tensor):
+    """(bf16 copy as int16 storage, fp32 row norms rounded up) of an fp32 [n, d] matrix:
+    the operands of lg_score_chunk_bound."""
+    x = _f32(x, "x")
+    xb = torch.empty(x.shape, dtype=torch.int16, device=x.device)
+    nrm = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    N.check(N.lib().lg_bound_prep_f32(N.ptr(x), x.shape[0], x.shape[1], N.ptr(xb), N.ptr(nrm),
+                                      N.stream_handle(x.device)), "lg_bound_prep_f32")
+    return xb, nrm
+
+
+def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """[users, ceil(width/64)] fp32 upper bounds of the fp32 score chain over each 64-column
+    chunk of items [j0, j0 + width) (lg_score_chunk_bound)."""
+    n = ub.shape[0]
+    nch = -(-width // 64)
+    if out is None or out.numel() < n * nch:
+        out = torch.empty(n * nch, dtype=torch.float32, device=ub.device)
+    gb = out[:n * nch].view(n, nch)
+    N.check(N.lib().lg_score_chunk_bound(N.ptr(ub), N.ptr(un), n, N.ptr(ib), N.ptr(inorm),
+                                         int(dim), int(j0), int(width), N.ptr(gb),
+                                         N.stream_handle(ub.device)), "lg_score_chunk_bound")
+    return gb
+
+
+class TileWalk:
+    """The fused top-K walk of users [u0, u1) over W tiles (lg_spread_tile_resource_topk_f64
+    per tile, with lg_score_chunk_bound screening when there is a G factor). Holds the
+    running lists (vals fp64 / idxs int64 [n, k]), the per-user exclusion cursors and the
+    bf16 score operands, so several walks (a lambda sweep) can share them."""
+
+    def __init__(self, A: Interactions, u0: int, u1: int, i0: int, k: int,
+                 ex: RowSets | None, eu=None, ei=None, tile: int = 2048):
+        self.A, self.u0, self.u1, self.i0, self.k, self.ex = A, u0, u1, i0, int(k), ex
+        self.n = u1 - u0
+        self.dev = A.k_item.device
+        self.vals = torch.full((self.n, self.k), float("-inf"), dtype=torch.float64,
+                               device=self.dev)
+        self.idxs = torch.full((self.n, self.k), -1, dtype=torch.int64, device=self.dev)
+        self.d = 0
+        self.eu = self.ei = None
+        if eu is not None:
+            self.eu, self.ei = _f32(eu, "eu"), _f32(ei, "ei")
+            self.d = self.eu.shape[1]
+            self.ub, self.un = bound_operands(self.eu)
+            self.ib, self.inorm = bound_operands(self.ei)
+            self.gbuf = torch.empty(self.n * -(-int(tile) // 64), dtype=torch.float32,
+                                    device=self.dev)
+        self.ex_cur = None
+        if ex is not None:
+            self.ex_cur = torch.empty(self.n, dtype=torch.int64, device=self.dev)
+        self.reset()
+
+    def reset(self) -> None:
+        """Empty lists; exclusion cursors back at the walk's first item."""
+        self.vals.fill_(float("-inf"))
+        self.idxs.fill_(-1)
+        if self.ex is not None:
+            N.check(N.lib().lg_spread_tile_seek(N.ptr(self.ex.rowptr), N.ptr(self.ex.col),
+                                                self.n, self.i0, N.ptr(self.ex_cur),
+                                                N.stream_handle(self.dev)),
+                    "lg_spread_tile_seek")
+
+    def bounds(self, j0: int, width: int) -> torch.Tensor | None:
+        if not self.d:
+            return None
+        return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
+                            self.gbuf)
+
+    def step(self, meta, ent, beta, inv_cls, j0: int, tile: int, width: int, first: bool,
+             gb: torch.Tensor | None = None) -> None:
+        """Merge tile [j0, j0 + width) (its W rows: meta / ent) into the lists."""
+        A, ex = self.A, self.ex
+        if self.d and gb is None:
+            gb = self.bounds(j0, width)
+        nch = gb.shape[1] if gb is not None else 0
+        N.check(N.lib().lg_spread_tile_resource_topk_f64(
+            N.ptr(A.by_user.rowptr[self.u0:]), N.ptr(A.by_user.col), self.n, N.ptr(meta),
+            N.ptr(ent), N.ptr(beta), N.ptr(inv_cls), int(j0), int(tile), int(width),
+            N.ptr(self.eu), N.ptr(self.ei), self.d, N.ptr(gb), nch,
+            N.ptr(ex.rowptr if ex is not None else None),
+            N.ptr(ex.col if ex is not None else None), N.ptr(self.ex_cur), self.k,
+            int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), N.stream_handle(self.dev)),
+            "lg_spread_tile_resource_topk_f64")
+
+
 def _fused_walk(A: Interactions, tw: TileWeights, u0: int, u1: int, i0: int, i1: int, k: int,
                 ex: RowSets | None, eu, ei, vals: torch.Tensor, idxs: torch.Tensor) -> None:
-    """Tiles [i0, i1) of the factored spreading with the top-K merge fused into the resource
-    pass (one lg_spread_tile_resource_topk_f64 per tile)."""
-    n = u1 - u0
-    dev = vals.device
-    strm = N.stream_handle(dev)
-    d, norms = 0, None
-    if eu is not None:
-        eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
-        d = eu.shape[1]
-        norms = row_norms(ei)
-    ex_cur = None
-    if ex is not None:
-        ex_cur = torch.empty(n, dtype=torch.int64, device=dev)
-        N.check(N.lib().lg_spread_tile_seek(N.ptr(ex.rowptr), N.ptr(ex.col), n, i0,
-                                            N.ptr(ex_cur), strm), "lg_spread_tile_seek")
-    rp = A.by_user.rowptr[u0:]
+    """Tiles [i0, i1) of the factored spreading with the top-K merge fused into the walk
+    (one lg_score_chunk_bound + lg_spread_tile_resource_topk_f64 per tile)."""
+    walk = TileWalk(A, u0, u1, i0, k, ex, eu, ei, tw.tile)
     for j0 in range(i0, i1, tw.tile):
         tw.build(j0, stop=i1)
-        N.check(N.lib().lg_spread_tile_resource_topk_f64(
-            N.ptr(rp), N.ptr(A.by_user.col), n, N.ptr(tw.meta), N.ptr(tw.ent), j0, tw.tile,
-            tw.width, N.ptr(eu), N.ptr(ei), d, N.ptr(norms),
-            N.ptr(ex.rowptr if ex is not None else None), N.ptr(ex.col if ex is not None else None),
-            N.ptr(ex_cur), int(k), int(j0 == i0), N.ptr(vals), N.ptr(idxs), strm),
-            "lg_spread_tile_resource_topk_f64")
+        walk.step(tw.meta, tw.ent, tw.beta, tw.inv_cls, j0, tw.tile, tw.width, j0 == i0)
+    vals.copy_(walk.vals)
+    idxs.copy_(walk.idxs)
+
+
+def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
+                        drop: bool = True, eu: torch.Tensor | None = None,
+                        ei: torch.Tensor | None = None, tiled: bool | None = None,
+                        tile: int = 2048, cache_bytes: int | None = None):
+    """Yield (lam, values [U, k] fp64, items [U, k] int64) of spread_recommend for every
+    lam of ``lams`` (the loop of findLambda.py:93-114: HybridS -> A @ W -> G * F -> top-k per
+    lambda), reusing what does not depend on lambda:
+      dense  general_W (lg_spread_general_f64) once; per lambda W (lg_hybrid_weight_f64) and
+             the fused F / top-k.
+      tiled  the W tiles hold only lambda-independent data (the (user, item) pair slots and
+             hub rows' general_W sums; alpha_i = k_i^(1-lam) sits in RowMeta and beta_j in
+             the walk's LDS table), so the tiles and the score bounds are built once and
+             cached on the device while they fit ``cache_bytes`` (default: half the free
+             memory); per lambda only alpha / beta change. If the cache does not fit, each
+             lambda rebuilds the tiles.
+    Every result is bitwise the one spread_recommend(A, lam, ...) returns."""
+    lams = [float(x) for x in lams]
+    dev = A.k_item.device
+    if tiled is None:
+        tiled = not dense_spread_fits(A.n_items, dev)
+    if not tiled:
+        gW = spread_general(A)
+        for lam in lams:
+            W = hybrid_weight(gW, A.k_item, lam)
+            v, i = spread_topk(A, W, k, excl, drop, eu, ei)
+            del W
+            yield lam, v, i
+        return
+    if cache_bytes is None:
+        cache_bytes = torch.cuda.mem_get_info(dev)[0] // 2
+    U, I = A.n_users, A.n_items
+    tile = min(int(tile), I) if I else 1
+    ex = excl if drop else None
+    walk = TileWalk(A, 0, U, 0, k, ex, eu, ei, tile)
+    cache, used, cached = [], 0, True
+    for n, lam in enumerate(lams):
+        alpha, beta = hybrid_factors(A.k_item, lam)
+        walk.reset()
+        if n > 0 and cached:
+            for (j0, width, meta, ent, gb) in cache:
+                meta[:, 1].copy_(alpha.view(torch.int64))
+                walk.step(meta, ent, beta, inv_cls, j0, tile, width, j0 == 0, gb)
+        else:
+            tw = TileWeights(A, lam, tile)
+            inv_cls = tw.inv_cls
+            for j0 in range(0, I, tile):
+                tw.build(j0)
+                gb = walk.bounds(j0, tw.width)
+                walk.step(tw.meta, tw.ent, tw.beta, tw.inv_cls, j0, tile, tw.width, j0 == 0,
+                          gb)
+                if n == 0 and cached and len(lams) > 1:
+                    total = int(tw.ptr[-1])
+                    need = total * 4 + tw.meta.numel() * 8 + (gb.numel() * 4 if gb is not None else 0)
+                    if used + need <= cache_bytes:
+                        cache.append((j0, tw.width, tw.meta.clone(), tw.ent[:total].clone(),
+                                      None if gb is None else gb.clone()))
+                        used += need
+                    else:
+                        cached = False
+                        cache.clear()
+            del tw
+        yield lam, walk.vals.clone(), walk.idxs.clone()
 
 
 def merge_topk_lists(vals: torch.Tensor, idxs: torch.Tensor):

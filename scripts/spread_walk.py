@@ -16,19 +16,28 @@ from lgcnhs import ops  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--tiles", type=int, default=16)
 ap.add_argument("--tile", type=int, default=2048)
+ap.add_argument("--workload", default="c5-d64")
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--unfused", action="store_true")
+ap.add_argument("--no-g", action="store_true", help="no G factor (SpreadMethod)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-U, I, E, D, _ = bench.WORKLOADS["c5-d64"]
+U, I, E, D, _ = bench.WORKLOADS[a.workload]
 _, _, keys = bench.gen_graph(U, I, E, 0, dev)
 A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
 del keys
 g = torch.Generator(device=dev).manual_seed(42)
 eu = torch.randn(U, D, device=dev, generator=g) * 0.1
 ei = torch.randn(I, D, device=dev, generator=g) * 0.1
-for rep in range(2):
+kw = {} if a.no_g else {"eu": eu, "ei": ei}
+for rep in range(a.reps):
     torch.cuda.synchronize()
     t = time.time()
-    ops.spread_topk_tiled(A, 0.5, 20, A.by_user, eu=eu, ei=ei, tile=a.tile,
-                          items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30)
+    st = {}
+    ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile, fused=not a.unfused,
+                          items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30,
+                          stats=st if rep == 0 else None, **kw)
     torch.cuda.synchronize()
-    print(f"rep {rep}: {a.tiles} tiles x {U} users: {time.time() - t:.3f} s", flush=True)
+    dt = time.time() - t
+    print(f"rep {rep}: {a.tiles} tiles x {U} users: {dt:.3f} s"
+          + (f"  slots {st['w_slots_read']:.3e}" if st else ""), flush=True)

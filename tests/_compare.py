@@ -4,10 +4,12 @@ may differ only where the k-th and (k+1)-th values are within `tol`."""
 import numpy as np
 
 
-def compare_topk_sets(got, ref, gaps=None, tol=0.0, max_tie_frac=0.01):
+def compare_topk_sets(got, ref, gaps=None, tol=0.0, max_tie_frac=0.01, got_vals=None):
     """got/ref: [U, k] int arrays (-1 = padding). gaps: [U, 2] = (v_k, v_k+1) of the
     reference row (NaN second entry: fewer than k+1 candidates). Returns the number of
-    tie-affected users; raises AssertionError on any other difference."""
+    tie-affected users; raises AssertionError on any other difference. With got_vals
+    ([U, k] values of got), a tie-affected user must still agree above the tie: the m items
+    of got whose values exceed v_k + tol are the reference's first m items (as sets)."""
     got = np.asarray(got)
     ref = np.asarray(ref)
     assert got.shape == ref.shape, (got.shape, ref.shape)
@@ -18,6 +20,11 @@ def compare_topk_sets(got, ref, gaps=None, tol=0.0, max_tie_frac=0.01):
         if g == r:
             continue
         if gaps is not None and not np.isnan(gaps[u, 1]) and abs(gaps[u, 0] - gaps[u, 1]) <= tol:
+            if got_vals is not None:
+                m = int(np.sum(np.asarray(got_vals[u]) > gaps[u, 0] + tol))
+                if set(got[u][:m].tolist()) != set(ref[u][:m].tolist()):
+                    bad.append((u, "above the tie", got[u][:m].tolist(), ref[u][:m].tolist()))
+                    continue
             ties += 1
             continue
         bad.append((u, sorted(g - r), sorted(r - g)))

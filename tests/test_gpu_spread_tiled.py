@@ -20,15 +20,11 @@ def _inter(U, I, n, seed, zipf=False):
 
 
 def _dense_tile(tw, I):
-    """The current tile of W as a dense [I, width] matrix (zeros where no entry)."""
-    ptr, ln = tw.ptr.cpu().numpy(), tw.len.cpu().numpy()
-    col, val = tw.col.cpu().numpy(), tw.val.cpu().numpy()
-    out = np.zeros((I, tw.width))
-    for i in range(I):
-        c = col[ptr[i]:ptr[i] + ln[i]]
-        assert np.all(np.diff(c) > 0), "row entries must be ascending and unique"
-        assert np.all((c >= tw.j0) & (c < tw.j0 + tw.width))
-        out[i, c - tw.j0] = val[ptr[i]:ptr[i] + ln[i]]
+    """The current tile of W as a dense [I, width] matrix (zeros where no entry), decoded
+    from the slot format with the walk's own arithmetic (TileWeights.dense checks the
+    format invariants: ascending columns, run flags, hub triples)."""
+    out = tw.dense()
+    assert out.shape == (I, tw.width)
     return out
 
 
@@ -245,24 +241,31 @@ def test_fused_dims_and_wide_k(d, k):
 
 @pytest.mark.parametrize("fused", [False, True])
 def test_spread_stats_count_path_updates(fused):
-    """stats["w_entries_read"] = sum over the users' items of the W row lengths inside the
-    item range = the nonzero path updates of F = A W (dense general_W nonzeros)."""
+    """stats["w_slots_read"] = sum over the users' items of the W row lengths inside each
+    tile of the item range: a P row holds one slot per (user, item) pair behind it (the
+    co-occurrence counts of the row, A^T A), a hub row (> 256 pairs) one triple per distinct
+    column."""
     from lgcnhs import ops
     U, I = 150, 400
     A = _inter(U, I, 3000, seed=3, zipf=True)
-    gW = ops.spread_general(A).cpu().numpy()
-    deg_rows = (gW != 0)
     Ad = np.zeros((U, I))
     rp, col = A.by_user.rowptr.cpu().numpy(), A.by_user.col.cpu().numpy()
     for u in range(U):
         Ad[u, col[rp[u]:rp[u + 1]]] = 1
+    C = Ad.T @ Ad  # pairs behind W[i][j]
     for users, items in ((slice(0, U), slice(0, I)), (slice(20, 90), slice(77, 301))):
         st = {}
         ops.spread_topk_tiled(A, 0.5, 10, A.by_user, tile=64, users=users, items=items,
                               fused=fused, stats=st)
         uses = Ad[users].sum(0)
-        want = int((uses[:, None] * deg_rows[:, items]).sum())
-        assert st["w_entries_read"] == want
+        want = 0
+        for j0 in range(items.start, items.stop, 64):
+            blk = C[:, j0:min(items.stop, j0 + 64)]
+            pairs = blk.sum(1)
+            slots = np.where(pairs <= 256, pairs, 3 * (blk != 0).sum(1))
+            want += int((uses * slots).sum())
+        assert st["w_slots_read"] == want
+    assert (C.sum(1) > 256).any(), "the zipf graph should have hub rows"
 
 
 @pytest.mark.parametrize("zipf", [False, True])
@@ -299,3 +302,44 @@ def test_tile_resource_persistent_waves_bitwise(zipf):
     tw2.resource(1000, 3500, Fb2)
     assert np.array_equal(Fb2[:, :tw2.width].cpu().numpy().view(np.uint64),
                           F[1000:3500, :tw2.width].view(np.uint64))
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_lambda_sweep_equals_per_lambda_recommend(tiled):
+    """spread_lambda_sweep (findLambda.py's loop with general_W / the W tiles and score
+    bounds built once) gives, for every lambda, spread_recommend's lists bit for bit; the
+    tiled sweep also with a cache too small to hold the tiles (rebuild per lambda)."""
+    from lgcnhs import ops
+    U, I, d = 240, 700, 64
+    A = _inter(U, I, 9000, seed=13, zipf=True)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
+    ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
+    lams = [0.0, 0.31, 0.5, 0.85, 1.0]
+    caches = (None, 1) if tiled else (None,)
+    for cache in caches:
+        got = list(ops.spread_lambda_sweep(A, lams, 12, A.by_user, True, eu, ei, tiled=tiled,
+                                           tile=128, cache_bytes=cache))
+        assert [g_[0] for g_ in got] == lams
+        for lam, v, i in got:
+            rv, ri = (ops.spread_topk_tiled(A, lam, 12, A.by_user, True, eu, ei, tile=128)
+                      if tiled else ops.spread_recommend(A, lam, 12, A.by_user, True, eu, ei,
+                                                         tiled=False))
+            assert torch.equal(i, ri), (lam, cache)
+            assert torch.equal(v.view(torch.int64), rv.view(torch.int64)), (lam, cache)
+
+
+def test_find_lambda_api_rows(tmp_path):
+    """findLambda.sweep_lambdas: one metrics row per lambda with the reference's columns."""
+    import pandas as pd
+    from lgcnhs.synth import synth_dataframes
+    from model.LightGCN.model import LightGCN
+    from findLambda import sweep_lambdas
+    _, tr, va, te = synth_dataframes(150, 300, 5000, seed=6, dist="zipf")
+    torch.manual_seed(42)
+    m = LightGCN(150, 300, 64, 3).to(DEV)
+    df = sweep_lambdas(m, 150, 300, tr, va, te, 10, lambdas=[0.0, 0.5, 1.0])
+    assert list(df.columns) == ["lambda", "precision", "recall", "f1", "ndcg", "H", "I"]
+    assert list(df["lambda"]) == [0.0, 0.5, 1.0]
+    assert df[["precision", "recall", "H", "I"]].notna().all().all()
+    del pd
