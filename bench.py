@@ -423,17 +423,17 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    st = {}  # W entries gathered by the resource passes (= path updates of F = A W)
+    st = {}  # paths added / row bytes gathered by the walk (the 3-hop paths of F = A W)
     (u0, u1), _, idx = sharded_spread_topk(A, lam, k, A.by_user, True, eu, ei, rank=rank,
                                            world=world, tile=tile, scratch_bytes=32 << 30,
                                            stats=st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    entries = float(st.get("w_slots_read", 0))
+    paths, nbytes = float(st.get("w_paths", 0)), float(st.get("w_bytes", 0))
     if world > 1:
-        e = torch.tensor([entries], dtype=torch.float64, device=dev)
+        e = torch.tensor([paths, nbytes], dtype=torch.float64, device=dev)
         dist.all_reduce(e)
-        entries = float(e.item())
+        paths, nbytes = float(e[0]), float(e[1])
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -447,12 +447,12 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     del A, idx
     torch.cuda.empty_cache()
     res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
-           "w_slots_per_s": entries / dt,
-           "w_slot_GBps": entries * 4 / dt / 1e9,
+           "paths_per_s": paths / dt,
+           "row_bytes_GBps": nbytes / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
-           "path": "lg_spread_tile_{seek,cursor,bound,weight,resource}_f64 + lg_tile_topk_f64 "
-                   "(G by f32 MFMA) + lg_topk_lists_merge_f64",
+           "path": "lg_spread_tile_{seek,cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
+                   "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64",
            "eval": evaluation}
     if world == 1:
         # configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), dense

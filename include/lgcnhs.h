@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 6
+#define LG_ABI_VERSION 7
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -200,16 +200,19 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
 
 /* ------------------------------------------------------------------------------------
  * Factored spreading over item tiles: the path for catalogs whose I x I general_W / W do
- * not fit (SURVEY.md §8 a9 "K3s"; C5 = 1M x 1M would need 8 TB per matrix). Same values,
- * bit for bit, as lg_spread_general_f64 -> lg_hybrid_weight_f64 -> lg_spread_resource_f64
+ * not fit (SURVEY.md §8 a9 "K3s"; C5 = 1M x 1M would need 8 TB per matrix). The values of
+ * lg_spread_general_f64 -> lg_hybrid_weight_f64 -> lg_spread_resource_f64
  * (-> lg_rows_topk_f64), i.e. the reference's getSpreadingGeneralMat / HybridS /
  * getResource / recommendForAllUser (model/SpreadMethod/model.py:14-99,
  * model/SpreadMethod/recommend.py:31-50, model/SpreadLightGCN/model.py:151), without ever
- * holding an I x I or U x I matrix. For each tile [j0, j0 + tile) of item columns the
+ * holding an I x I or U x I matrix, as
+ *   F[u][j] = rb_j * sum over the paths u -> i -> v -> j of fl(1/k_v) * ra_i
+ * (ra = 1/alpha, rb = 1/beta; each term within a few ulp of the reference's W entry, the
+ * summation order the walk's own, fixed). For each tile [j0, j0 + tile) of item columns the
  * caller runs: lg_spread_tile_cursor -> lg_spread_tile_bound -> (exclusive prefix of the
- * bounds = wt_ptr) -> lg_spread_tile_weight_f64 -> lg_spread_tile_resource_f64 per block
- * of users -> lg_tile_topk_f64. The orchestration (lgcnhs.ops.spread_topk_tiled) is host
- * code; see DESIGN.md §5 K3s.
+ * rows' overflow units = ovf_ptr) -> lg_spread_tile_rows_f64 -> lg_spread_tile_resource_f64
+ * (F) or lg_spread_tile_resource_topk_f64 (running top-K lists). The orchestration
+ * (lgcnhs.ops.spread_topk_tiled) is host code; see DESIGN.md §5 K3s.
  * ------------------------------------------------------------------------------------ */
 
 /* alpha[i] = k_item[i]^(1 - lambda), beta[i] = k_item[i]^lambda: the HybridS degree
@@ -217,6 +220,11 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
  * lg_hybrid_weight_f64. */
 int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
                           double *alpha, double *beta, lg_stream_t stream);
+
+/* ra[i] = 1 / alpha[i], rb[i] = 1 / beta[i] (a zero factor -> 1: the reference's den == 0
+ * rule, model/SpreadMethod/model.py:81-82; such rows / columns hold no paths). */
+int lg_hybrid_recip_f64(const double *k_item, int64_t n_items, double lambda, double *ra,
+                        double *rb, lg_stream_t stream);
 
 /* inv[v] = fl(1 / (rowptr[v+1] - rowptr[v])): the (A.T / k_u) factor of
  * model/SpreadMethod/model.py:21-25, as lg_spread_general_f64 computes it. */
@@ -233,48 +241,54 @@ int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                           int64_t *end, uint16_t *count, lg_stream_t stream);
 
 /* bound[i] = sum over users v of item i (item_rowptr/item_users) of count[v]: the number of
- * (user, tile item) pairs behind W's row i in the tile, an upper bound on its entries. */
+ * (user, tile item) pairs behind W's row i in the tile (its paths). */
 int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
                          int64_t n_items, const uint16_t *count, int64_t *bound,
                          lg_stream_t stream);
 
-/* Row i of W restricted to the tile, for every item i, where
- *   W[i][j] = (sum_{v in users(i) and users(j), ascending v} fl(1/k_v))
- *             / (alpha[i] * beta[j])          (den == 0 -> 1),
- * stored at wt_ent[wt_ptr[i] ..] (4-byte slots) in one of two formats:
- *   P rows (bound[i] <= 256 pairs): one slot per (user v, item j) pair, sorted by (j, v):
- *     bits 0-15 j - item_begin, bits 16-29 user_cls[v] (the class of v's degree:
- *     inv_cls[user_cls[v]] = fl(1/k_v)), bit 30 "next slot same column", bit 31 "previous
- *     slot same column"; the walk forms each path's W value from these (same bits);
- *   V rows (hub items, bound[i] > 256): one 12-byte triple per distinct column,
- *     {(0x3FFF << 16) | (j - item_begin), fp64 W value as lo, hi}.
- * wt_meta[i] = {ptr | len << 40 | V << 63, alpha[i]} (16 bytes; len in slots). wt_ptr is
- * the caller's prefix of row capacities (in slots): bound[i] for P rows,
- * 3 * min(bound[i], tile) for V rows, each rounded up to a multiple of 32 slots so rows
- * start on 128-byte lines. cur/count from lg_spread_tile_cursor, bound from
- * lg_spread_tile_bound, inv_deg from lg_inv_degree_f64 over the user rows (V rows), user_cls
- * one uint16 class per user (< 16383 classes). ws: lg_spread_tile_weight_ws_bytes(n_items)
- * bytes of scratch. tile in [1, 8192]; every item of the tile lies in
- * [item_begin, item_begin + tile). */
-size_t lg_spread_tile_weight_ws_bytes(int64_t n_items);
-int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                              const int32_t *user_items, const uint16_t *user_cls,
-                              const double *inv_deg, int64_t n_items, const int64_t *cur,
-                              const uint16_t *count, const double *alpha, const double *beta,
-                              int32_t item_begin, int32_t tile, const int64_t *bound,
-                              const int64_t *wt_ptr, void *wt_ent, void *wt_meta, void *ws,
-                              size_t ws_bytes, lg_stream_t stream);
+/* Row i of general_W restricted to the tile, for every item i, as one 128-byte line at
+ * lines + 128 i (32 uint32 words) plus, for rows that do not fit, a run of 16-byte units in
+ * ovf. Word 0 = header: bit 31 V format, bit 30 overflow, bits 0-28 the run's first unit
+ * (whose .x = the number of data units after it).
+ *   P rows (bound[i] <= vthr): one word per (user v, item j) pair behind the row, users
+ *     ascending then items ascending: bits 0-15 j - item_begin, bits 16-30 user_cls[v] (a
+ *     1-based class of v's degree, < 0x8000: inv_cls[user_cls[v]] = fl(1/k_v)); 0 =
+ *     padding; bit 31 clear. Line words 1-31 then 4 per data unit.
+ *   V rows (hub items, bound[i] > vthr): one 16-byte entry per distinct column, ascending:
+ *     {0x80000000 | (j - item_begin), fp64 general_W[i][j] (lo, hi), 0}. Line units 1-7 then
+ *     1 per data unit.
+ * ovf_ptr[i] = the caller's exclusive prefix over rows of their overflow units:
+ * 1 + ceil((bound - 31) / 4) for P rows with bound > 31, 1 + (min(bound, tile) - 7) for V
+ * rows with min(bound, tile) > 7, else 0; ovf must hold that total + 64 units (the walk
+ * reads 64 units per run). row_len[i] (optional) = the row's pairs (P) or entries (V).
+ * Header bit 29 ("slow") marks V rows and P rows with a class >= 512 (the walk's general
+ * decode); the overflow pointer has 29 bits. Lambda-independent (a sweep reuses the tile).
+ * Line n_items (the walk's padding row) is never written: the caller zeroes it. cur/count from lg_spread_tile_cursor, bound
+ * from lg_spread_tile_bound, inv_deg from lg_inv_degree_f64 over the user rows (V rows).
+ * ws: lg_spread_tile_rows_ws_bytes(n_items) bytes of scratch. tile in [1, 8192];
+ * vthr >= 31; every item of the tile lies in [item_begin, item_begin + tile). */
+size_t lg_spread_tile_rows_ws_bytes(int64_t n_items);
+int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                            const int32_t *user_items, const uint16_t *user_cls,
+                            const double *inv_deg, int64_t n_items, const int64_t *cur,
+                            const uint16_t *count, int32_t item_begin, int32_t tile,
+                            const int64_t *bound, int64_t vthr, const int64_t *ovf_ptr,
+                            void *lines, void *ovf, int32_t *row_len, void *ws,
+                            size_t ws_bytes, lg_stream_t stream);
 
-/* F[u][j - item_begin] = sum_{i in items(u), ascending} W[i][j] for the n_users rows of
- * user_rowptr (pass user_rowptr + u0 for a block) and j in [item_begin, item_begin + tile)
- * (columns >= item_begin + width are 0); F row-major with leading dim ldf >= tile;
- * wt_meta / wt_ent from lg_spread_tile_weight_f64, beta = all items' beta, inv_cls the
- * degree-class table. */
+/* F[u][j - item_begin] = rb[j] * sum over the paths of u's items of the tile's rows (see the
+ * section comment) for the n_users rows of user_rowptr (pass user_rowptr + u0 for a block)
+ * and j in [item_begin, item_begin + tile) (columns >= item_begin + width are 0); F
+ * row-major with leading dim ldf >= tile. ra_edge[p] = ra[user_items[p]] (aligned with
+ * user_items, at least one entry), rbeta = rb of all items, inv_cls the class table;
+ * lines / ovf from lg_spread_tile_rows_f64, with line null_row (= n_items: lines holds
+ * n_items + 1) all zero. */
 int lg_spread_tile_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                int64_t n_users, const void *wt_meta, const void *wt_ent,
-                                const double *beta, const double *inv_cls, int32_t item_begin,
-                                int32_t tile, int32_t width, double *F, int64_t ldf,
-                                lg_stream_t stream);
+                                const double *ra_edge, int64_t n_users, const void *lines,
+                                const void *ovf, int32_t null_row, const double *rbeta,
+                                const double *inv_cls,
+                                int32_t item_begin, int32_t tile, int32_t width, double *F,
+                                int64_t ldf, lg_stream_t stream);
 
 /* Merge columns [item_begin, item_begin + n_cols) of (G *) F (F[r][0..n_cols), leading dim
  * ldf; G as in lg_rows_topk_f64 with eu = the rows' user embeddings and ei = all item
@@ -303,24 +317,26 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
                             lg_stream_t stream);
 
 /* Fused lg_spread_tile_resource_f64 + lg_tile_topk_f64 for one tile: each user's F columns
- * [item_begin, item_begin + width) are accumulated in LDS (same values, bit for bit) and
- * merged straight into the running top-K lists io_val/io_idx [n_users][k] (first != 0:
- * start empty); F is never written to memory. G factor: eu = the rows' user embeddings,
- * ei = all item embeddings, gb = lg_score_chunk_bound's [n_users][n_chunks] bounds for this
- * tile (n_chunks = ceil(width / 64)): only columns with gb * F > the K-th value get the exact
- * score chain. Exclusions (dropped): ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row
- * cursor ex_cur[n_users] positioned at the walk's first item by
- * lg_spread_tile_seek(ex_rowptr, ex_col, ...) and advanced here. Walked over tiles in
- * ascending order, the lists equal lg_rows_topk_f64 over the full rows. k in [1, 128]; dim
- * in {32, 64, 128}. lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
+ * [item_begin, item_begin + width) are accumulated in LDS (the values lg_spread_tile_
+ * resource_f64 writes, bit for bit) and merged straight into the running top-K lists
+ * io_val/io_idx [n_users][k] (first != 0: start empty); F is never written to memory. G
+ * factor: eu = the rows' user embeddings, ei = all item embeddings, gb =
+ * lg_score_chunk_bound's [n_users][n_chunks] bounds for this tile (n_chunks =
+ * ceil(width / 64) <= 64): only columns with gb * F > the K-th value get the exact score chain.
+ * Exclusions (dropped): ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row cursor
+ * ex_cur[n_users] positioned at the walk's first item by lg_spread_tile_seek(ex_rowptr,
+ * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
+ * lg_tile_topk_f64 over lg_spread_tile_resource_f64's tiles. k in [1, 128]; dim in
+ * {32, 64, 128}. lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
  * workgroup's tables (the launch fits as many waves per CU as the LDS holds). */
 size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
 int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                     int64_t n_users, const void *wt_meta, const void *wt_ent,
-                                     const double *beta, const double *inv_cls,
-                                     int32_t item_begin, int32_t tile, int32_t width,
-                                     const float *eu, const float *ei, int32_t dim,
-                                     const float *gb, int32_t n_chunks,
+                                     const double *ra_edge, int64_t n_users,
+                                     const void *lines, const void *ovf, int32_t null_row,
+                                     const double *rbeta,
+                                     const double *inv_cls, int32_t item_begin, int32_t tile,
+                                     int32_t width, const float *eu, const float *ei,
+                                     int32_t dim, const float *gb, int32_t n_chunks,
                                      const int64_t *ex_rowptr, const int32_t *ex_col,
                                      int64_t *ex_cur, int32_t k, int32_t first,
                                      double *io_val, int64_t *io_idx, lg_stream_t stream);

@@ -8,22 +8,30 @@
 //   F_new = G * F; per user argsort desc, drop train|val, [:k]
 //                       model/SpreadLightGCN/model.py:151, recommend.py:18-52
 //
+// Factored: W[i][j] = general_W[i][j] * ra_i * rb_j with ra = 1/alpha, rb = 1/beta (alpha_i =
+// k_i^(1-l), beta_j = k_j^l; a zero factor -> 1, the reference's den == 0 rule), so
+//   F[u][j] = rb_j * sum_{i in items(u)} ra_i * sum_{v in users(i) and users(j)} fl(1/k_v)
+//           = rb_j * sum over the 3-hop paths u -> i -> v -> j of fl(1/k_v) * ra_i.
 // The items are processed in column tiles [j0, j0 + T). Per tile:
 //   cursor   end[v] = first position of user v's (ascending) item row with item >= j0 + T;
 //            cur[v] (the previous tile's end) marks the first item >= j0, so
 //            items(v) inside the tile = user_items[cur[v] .. end[v])
 //   bound    bound[i] = sum_{v in users(i)} (end[v] - cur[v]) = the (user, item) pairs
-//            behind row i of W in the tile
-//   weight   row i of W restricted to the tile (format below: the pairs themselves, 4 bytes
-//            each, for ordinary rows; merged fp64 values for hub rows)
-//   walk     per user: F[u][j - j0] = sum_{i in items(u), ascending} W[i][j] in an LDS
-//            accumulator (one wave per user, lg_spread_resource_f64's order and values), then
-//            either written out (F mode) or merged straight into the user's running top-K
-//            list (top-K mode: (G *) F, G = the fp32 e0 score chain, candidates screened by
-//            per-(user, 64-column chunk) score bounds from lg_score_chunk_bound).
-// Work: the weight pass costs sum_i deg(i) lookups + the 2-hop pairs once per tile (not per
-// user); the walk reads deg(u) short row segments per user and tile (~1e12 paths at C5:
-// 4 bytes per path, F never leaves LDS).
+//            behind row i of W in the tile (its paths)
+//   rows     row i of general_W restricted to the tile, in the line format below
+//   walk     per user (one wave): the paths of its rows added into an LDS accumulator, then
+//            scaled by rb_j and either written out (F mode) or merged straight into the
+//            user's running top-K list (top-K mode: (G *) F, G = the fp32 e0 score chain,
+//            candidates screened by per-(user, 64-column chunk) score bounds).
+// Work: the rows pass costs sum_i deg(i) lookups + the 2-hop pairs once per tile (not per
+// user); the walk reads one 128-byte line per (user, item) and tile (~5e10 lines at C5) and
+// adds ~1e12 paths (one LDS atomic each); F never leaves LDS.
+//
+// Rounding: every path contributes fl(fl(1/k_v) * ra_i) (P rows) or fl(general_W[i][j] * ra_i)
+// (V rows); the sum order is the walk's (fixed: deterministic, but not the dense path's
+// ascending-i order), then one multiply by rb_j. Against the reference's
+// general_W / (alpha (x) beta) summed by BLAS this is a few ulp per term (tests: 1e-12
+// relative), the reference's own BLAS order being unspecified.
 #include <stdlib.h>
 
 #include "common.h"
@@ -32,39 +40,36 @@ namespace lg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// A W tile is stored as one row segment per item i, in one of two formats (RowMeta, one
-// 16-byte load per row: m = ptr | len << 40 | V << 63, and alpha_i):
+// A W tile is one 128-byte LINE per item row i at lines[i * 32 ..] (32 words) plus, for rows
+// that do not fit, a run of 16-byte units in an overflow array. Word 0 of the line is the
+// header: bit 31 = V format, bit 30 = overflow, bit 29 = slow (a V row, or a P row with a
+// degree class >= kInvTab: the walk's general decode), bits 0-28 = the overflow run's first
+// unit (ovf[u].x = the number of data units that follow it). No per-row metadata: the walk
+// reads the line of every item of its user straight from i * 128. Line I (one past the last
+// item) is all zero: the walk's padding rows read it.
 //
-// P rows (<= kSortMax pairs, the common case): one 4-byte slot per (user v, item j) PAIR
-//   behind the row (v in users(i), j in items(v) inside the tile), sorted by (j, v):
+// P rows (<= the hub threshold's pairs, the common case): one 4-byte slot per (user v,
+//   item j) PAIR behind the row (v in users(i), j in items(v) inside the tile), in pair order
+//   (users ascending, each user's items ascending):
 //     bits 0-15  j - item_begin
-//     bits 16-29 the class of v's degree k_v (fl(1 / k_v) = inv[class], classes < kInvTab
-//                cached in LDS)
-//     bit 30     the next slot is the same column (a run of users of one (i, j))
-//     bit 31     this slot continues the previous slot's column
-//   The resource pass forms W[i][j] = (sum of the run's fl(1/k_v), ascending v) /
-//   (alpha_i * beta_j) per path: the sum of lg_spread_general_f64 and the division of
-//   lg_hybrid_weight_f64, bit for bit, without storing an fp64 per entry (4 bytes per path
-//   instead of 12; the path count, ~1e12 at C5, sets the runtime).
-// V rows (hub items, > kSortMax pairs, merged while building): one 12-byte triple per
-//   distinct column: slot 0 = (kClsV << 16) | (j - item_begin), slots 1-2 = the fp64
-//   general_W[i][j] (lo, hi), divided by alpha_i * beta_j in the walk like a P run.
-// Neither format depends on lambda (only RowMeta's alpha and the walk's beta table do), so
-// a lambda sweep reuses the built tiles.
-constexpr uint32_t kClsMask = 0x3FFF;
-constexpr uint32_t kClsV = 0x3FFF;         // class field of a V-row triple's first slot
-constexpr uint32_t kHasNext = 0x40000000u;
-constexpr uint32_t kIsCont = 0x80000000u;
-constexpr int kLenShift = 40;
-constexpr uint64_t kPtrMask = (1ull << kLenShift) - 1;
-constexpr uint64_t kLenMask = (1ull << 23) - 1;
-constexpr uint64_t kFmtV = 1ull << 63;
-constexpr int kInvTab = 512;  // degree classes whose fl(1/k) is cached in LDS
-
-struct RowMeta {
-  uint64_t m;
-  double alpha;
-};
+//     bits 16-30 the 1-based class of v's degree k_v (fl(1 / k_v) = inv[class]; classes
+//                < kInvTab are cached in LDS); bit 31 clear (it marks V entries); a zero
+//                word is padding
+//   line words 1..31 hold the first 31 slots, the overflow units 4 slots each.
+// V rows (hub items, more pairs than the threshold; merged while building): one 16-byte
+//   entry per distinct column, ascending: {0x80000000 | (j - item_begin), fp64
+//   general_W[i][j] (lo, hi), 0}; line units 1..7 hold the first 7, the overflow units one
+//   each.
+// Neither format depends on lambda (ra / rb are applied by the walk), so a lambda sweep
+// reuses the built tiles.
+constexpr uint32_t kHdrV = 0x80000000u;
+constexpr uint32_t kHdrOvf = 0x40000000u;
+constexpr uint32_t kHdrSlow = 0x20000000u;
+constexpr uint32_t kHdrPtr = 0x1FFFFFFFu;
+constexpr uint32_t kEntV = 0x80000000u;
+constexpr int kLineSlots = 31;  // P slots in a line (word 0 is the header)
+constexpr int kLineEnts = 7;    // V entries in a line (unit 0 holds the header)
+constexpr int kInvTab = 512;    // degree classes whose fl(1/k) is cached in LDS
 
 __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
                                                         int64_t n, double lambda,
@@ -141,72 +146,59 @@ __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ 
   if (lane == 0) bound[i] = s;
 }
 
-constexpr int kSortMax = 256;  // pairs per row handled by the in-wave sort (P rows)
-
-// Sort the n (<= 64*M) staged pairs (key = -item, id = staging position, which ascends
-// with the user) of this wave by (item, user) and write them as P slots.
-template <int M>
-__device__ __forceinline__ void sort_write_row(int *skey, int *sid, const uint16_t *scls, int n,
-                                               int64_t wbase, int32_t item_begin,
-                                               uint32_t *__restrict__ wt_ent) {
-  const int lane = lane_id();
-  int k[M], id[M];
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const int e = j * 64 + lane;
-    if (e < n) { k[j] = skey[e]; id[j] = sid[e]; }
-    else { k[j] = INT32_MIN; id[j] = kPadId; }
-  }
-  wave_sync();
-  // before(): key desc, id asc  ->  item asc, user asc; padding (INT32_MIN) last
-  wave_bitonic_sort<int, M>(k, id);
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const int e = j * 64 + lane;
-    skey[e] = k[j];
-    sid[e] = id[j];
-  }
-  wave_sync();
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const int e = j * 64 + lane;
-    if (e < n) {
-      const int key = skey[e];
-      const bool prv = e > 0 && skey[e - 1] == key;
-      const bool nxt = e + 1 < n && skey[e + 1] == key;
-      wt_ent[wbase + e] = (prv ? kIsCont : 0u) | (nxt ? kHasNext : 0u) |
-                          ((uint32_t)scls[sid[e]] << 16) | (uint32_t)(-key - item_begin);
-    }
-  }
+// ra[i] = 1 / k_item[i]^(1 - lambda), rb[i] = 1 / k_item[i]^lambda (the same pow() calls as
+// k_hybrid_weight); a zero factor -> 1 (its rows / columns hold no paths).
+__global__ __launch_bounds__(256) void k_hybrid_recip(const double *__restrict__ k_item,
+                                                      int64_t n, double lambda,
+                                                      double *__restrict__ ra,
+                                                      double *__restrict__ rb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = pow(k_item[i], 1.0 - lambda), b = pow(k_item[i], lambda);
+  ra[i] = a != 0.0 ? 1.0 / a : 1.0;
+  rb[i] = b != 0.0 ? 1.0 / b : 1.0;
 }
 
-// P rows: one wave per item row with bound[i] <= kSortMax pairs (LDS staging per wave).
-__global__ __launch_bounds__(256) void k_tile_weight(
+// ------------------------------------------------------------------- the rows pass
+// Slot p of a row: line word 1 + p for p < 31, else word (p - 31) of the overflow run's
+// data units (the run's unit 0 is its header).
+__device__ __forceinline__ void put_slot(uint32_t *__restrict__ line, uint32_t *__restrict__ ovf,
+                                         int64_t ou, int64_t p, uint32_t w) {
+  if (p < kLineSlots) line[1 + p] = w;
+  else ovf[(ou + 1) * 4 + (p - kLineSlots)] = w;
+}
+
+// P rows: one wave per item row with bound[i] <= vthr pairs. Every word of the line and of
+// the overflow run is written exactly once (header, pairs, zero padding), so no stale data
+// of an earlier tile survives and no two stores of the wave hit one word.
+__global__ __launch_bounds__(256) void k_tile_rows(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, const uint16_t *__restrict__ user_cls,
     int64_t n_items, const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
-    const double *__restrict__ alpha, int32_t item_begin, const int64_t *__restrict__ bound,
-    const int64_t *__restrict__ wt_ptr, uint32_t *__restrict__ wt_ent,
-    RowMeta *__restrict__ wt_meta) {
-  __shared__ int skey[4][kSortMax];
-  __shared__ int sid[4][kSortMax];
-  __shared__ uint16_t scls[4][kSortMax];
-  const int wave = threadIdx.x / 64;
-  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+    int32_t item_begin, const int64_t *__restrict__ bound, int64_t vthr,
+    const int64_t *__restrict__ ovf_ptr, uint32_t *__restrict__ lines,
+    uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   if (i >= n_items) return;
   const int lane = lane_id();
   const int64_t nb = bound[i];
-  if (nb > kSortMax) return;  // hub row: k_tile_weight_hub
-  const int64_t wbase = wt_ptr[i];
-  if (lane == 0) wt_meta[i] = RowMeta{(uint64_t)wbase | ((uint64_t)nb << kLenShift), alpha[i]};
-  if (nb == 0) return;
-  // stage the pairs: users of i in ascending order, each user's items inside the tile
-  int n = 0;
-  for (int64_t e0 = item_rowptr[i]; e0 < item_rowptr[i + 1]; e0 += 64) {
+  if (nb > vthr) return;  // hub row: k_tile_rows_hub
+  uint32_t *line = lines + i * 32;
+  const bool has_ovf = nb > kLineSlots;
+  const int64_t ou = has_ovf ? ovf_ptr[i] : 0;
+  const int64_t n_units = has_ovf ? (nb - kLineSlots + 3) / 4 : 0;
+  const int64_t cap = kLineSlots + 4 * n_units;
+  if (has_ovf && lane < 4) ovf[ou * 4 + lane] = lane == 0 ? (uint32_t)n_units : 0u;
+  for (int64_t p = nb + lane; p < cap; p += 64) put_slot(line, ovf, ou, p, 0u);
+  // the pairs: users of i ascending, each user's items in the tile ascending
+  int64_t n = 0;
+  bool far = false;
+  const int64_t e1 = item_rowptr[i + 1];
+  for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
     const int64_t e = e0 + lane;
     int32_t v = 0;
     int c = 0;
-    if (e < item_rowptr[i + 1]) {
+    if (e < e1) {
       v = item_users[e];
       c = count[v];
     }
@@ -220,36 +212,31 @@ __global__ __launch_bounds__(256) void k_tile_weight(
     pre -= c;
     if (c) {
       const int64_t s0 = cur[v];
-      const uint16_t cl = user_cls[v];
-      for (int q = 0; q < c; ++q) {
-        const int p = n + pre + q;
-        skey[wave][p] = -user_items[s0 + q];
-        sid[wave][p] = p;
-        scls[wave][p] = cl;
-      }
+      const uint32_t cl = (uint32_t)user_cls[v];
+      far |= cl >= (uint32_t)kInvTab;
+      for (int q = 0; q < c; ++q)
+        put_slot(line, ovf, ou, n + pre + q,
+                 (cl << 16) | (uint32_t)(user_items[s0 + q] - item_begin));
     }
     n += total;
   }
-  wave_sync();
-  if (n <= 64)
-    sort_write_row<1>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
-  else if (n <= 128)
-    sort_write_row<2>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
-  else
-    sort_write_row<4>(skey[wave], sid[wave], scls[wave], n, wbase, item_begin, wt_ent);
+  const bool slow = __ballot(far) != 0;
+  if (lane == 0) {
+    line[0] = (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u) | (slow ? kHdrSlow : 0u);
+    if (row_len) row_len[i] = (int32_t)nb;
+  }
 }
 
-// V rows (bound > kSortMax pairs, hub items): one 256-thread block per row (grid-stride
-// over the hub list), the tile as a dense LDS accumulator, users walked in ascending order
-// as in k_spread_general, then the touched columns written as merged triples.
-__global__ __launch_bounds__(256) void k_tile_weight_hub(
+// V rows (bound > vthr pairs, hub items): one 256-thread block per row (grid-stride over the
+// hub list), the tile as a dense LDS accumulator of general_W, users walked in ascending
+// order as in k_spread_general, then the touched columns written as ascending entries.
+__global__ __launch_bounds__(256) void k_tile_rows_hub(
     const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
-    const int64_t *__restrict__ cur, const uint16_t *__restrict__ count,
-    const double *__restrict__ alpha, const double *__restrict__ beta, int32_t item_begin,
-    int32_t tile, const int64_t *__restrict__ wt_ptr, uint32_t *__restrict__ wt_ent,
-    RowMeta *__restrict__ wt_meta) {
+    const int64_t *__restrict__ cur, const uint16_t *__restrict__ count, int32_t item_begin,
+    int32_t tile, const int64_t *__restrict__ ovf_ptr, uint32_t *__restrict__ lines,
+    uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
   extern __shared__ double acc[];  // tile doubles
   __shared__ int wsum[4];
   const int64_t nh = *n_hub;
@@ -266,9 +253,8 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
       for (int q = threadIdx.x; q < c; q += blockDim.x) acc[user_items[s0 + q] - item_begin] += wv;
       __syncthreads();  // the next user may hit the same columns from other threads
     }
-    // compact the touched columns (every contribution is > 0) in ascending order
-    const double a = alpha[i];
-    const int64_t wbase = wt_ptr[i];
+    uint32_t *line = lines + i * 32;
+    const int64_t ou = ovf_ptr[i];
     int base = 0;
     for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
       const int j = j0 + threadIdx.x;
@@ -284,223 +270,36 @@ __global__ __launch_bounds__(256) void k_tile_weight_hub(
       }
       if (nz) {
         const uint64_t bits = (uint64_t)__double_as_longlong(acc[j]);
-        const int64_t p = wbase + 3 * (int64_t)(base + before_w + __popcll(b & lanemask_lt()));
-        wt_ent[p] = (kClsV << 16) | (uint32_t)j;
-        wt_ent[p + 1] = (uint32_t)bits;
-        wt_ent[p + 2] = (uint32_t)(bits >> 32);
+        const int64_t e = base + before_w + __popcll(b & lanemask_lt());
+        uint32_t *u4 = e < kLineEnts ? line + 4 * (1 + e) : ovf + 4 * (ou + 1 + (e - kLineEnts));
+        *reinterpret_cast<uint4 *>(u4) =
+            uint4{kEntV | (uint32_t)j, (uint32_t)bits, (uint32_t)(bits >> 32), 0u};
       }
       base += total;
       __syncthreads();
     }
-    if (threadIdx.x == 0)
-      wt_meta[i] = RowMeta{(uint64_t)wbase | ((uint64_t)(3 * base) << kLenShift) | kFmtV, a};
+    // header, the unused line units, the overflow run's header
+    const bool has_ovf = base > kLineEnts;
+    if (threadIdx.x < 32) {
+      const int t = threadIdx.x;  // line word t
+      const int unit = t / 4;
+      if (t == 0) line[0] = kHdrV | kHdrSlow | (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u);
+      else if (unit == 0 || unit > base) line[t] = 0u;
+    }
+    if (has_ovf && threadIdx.x < 4)
+      ovf[ou * 4 + threadIdx.x] = threadIdx.x == 0 ? (uint32_t)(base - kLineEnts) : 0u;
+    if (threadIdx.x == 0 && row_len) row_len[i] = base;
     __syncthreads();
   }
 }
 
 __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ bound,
-                                                  int64_t n_items,
+                                                  int64_t n_items, int64_t vthr,
                                                   unsigned long long *__restrict__ n_hub,
                                                   int64_t *__restrict__ hub_rows) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
-  if (bound[i] > kSortMax) hub_rows[atomicAdd(n_hub, 1ull)] = i;
-}
-
-// ------------------------------------------------------------------ the resource pass
-// F[u][j] = sum over items(u) ascending of W[i][j]: one wave per user, the tile's
-// accumulator in LDS. A user's rows are taken 128 at a time: their RowMeta is fetched in one
-// round trip and indexed in LDS (empty rows dropped, inclusive slot prefix, slot base,
-// alpha_i); the rows' slots are then flattened: lane l takes slots e = e0 + q*64 + l of the
-// concatenated rows, UF loads in flight per lane, its row found by a short scan from the
-// previous register's last row (rows are non-empty, so 64 slots span at most 64 rows). Each
-// path's W value is formed in registers and added with ds_add_f64; adds of one instruction
-// that hit the same column come from rows in lane order and instructions go in slot order,
-// so each column receives its rows' values in ascending row order: the order of
-// lg_spread_resource_f64, hence the same bits.
-constexpr int kResRows = 128;
-struct RowIndex {
-  int cincl[kResRows];     // inclusive prefix of the rows' 4-slot chunks
-  int cexcl[kResRows];     // exclusive prefix
-  int len[kResRows];       // slots | 0x80000000 for V rows
-  int pad_[kResRows];
-  int64_t base[kResRows];  // the row's first slot
-  double alpha[kResRows];
-};
-
-// Index of a group of up to 128 rows (RowMeta of rows lane and 64 + lane), empty rows
-// dropped; returns the group's chunk count.
-__device__ __forceinline__ int write_row_index(RowIndex *ix, RowMeta m0, RowMeta m1) {
-  const int lane = lane_id();
-  const int l0 = (int)((m0.m >> kLenShift) & kLenMask), l1 = (int)((m1.m >> kLenShift) & kLenMask);
-  const int c0 = (l0 + 3) >> 2, c1 = (l1 + 3) >> 2;
-  int in0 = c0, in1 = c1;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y0 = __shfl_up(in0, o), y1 = __shfl_up(in1, o);
-    if (lane >= o) { in0 += y0; in1 += y1; }
-  }
-  in1 += __shfl(in0, 63);
-  const int total = __shfl(in1, 63);
-  const uint64_t b0 = __ballot(l0 > 0), b1 = __ballot(l1 > 0);
-  const int p0 = __popcll(b0 & lanemask_lt());
-  const int p1 = __popcll(b0) + __popcll(b1 & lanemask_lt());
-  wave_sync();  // earlier readers of this index are done
-  ix->cincl[lane] = 0x7fffffff;  // rows past the group's last (binary search sentinel)
-  ix->cincl[64 + lane] = 0x7fffffff;
-  wave_sync();
-  if (l0 > 0) {
-    ix->cincl[p0] = in0;
-    ix->cexcl[p0] = in0 - c0;
-    ix->len[p0] = l0 | ((int64_t)m0.m < 0 ? (int)0x80000000 : 0);
-    ix->base[p0] = (int64_t)(m0.m & kPtrMask);
-    ix->alpha[p0] = m0.alpha;
-  }
-  if (l1 > 0) {
-    ix->cincl[p1] = in1;
-    ix->cexcl[p1] = in1 - c1;
-    ix->len[p1] = l1 | ((int64_t)m1.m < 0 ? (int)0x80000000 : 0);
-    ix->base[p1] = (int64_t)(m1.m & kPtrMask);
-    ix->alpha[p1] = m1.alpha;
-  }
-  wave_sync();
-  return total;
-}
-
-__device__ __forceinline__ double inv_of(uint32_t x, const double *s_inv,
-                                         const double *__restrict__ g_inv) {
-  const uint32_t c = (x >> 16) & kClsMask;
-  return c < kInvTab ? s_inv[c] : g_inv[c];
-}
-
-// acc[j - item_begin] += the `total` flattened 4-slot chunks of one indexed row group.
-// Lane l loads chunk c0 + 64q + l (16 bytes: rows start on 128-byte lines and hold whole
-// chunks of capacity), its row found by UC lockstep binary searches over the group's chunk
-// prefix; each 256-slot register is then transposed through LDS into slot order, so
-// instruction t of it takes slots 64t .. 64t + 63 in lane order, the order that keeps every
-// column's adds in ascending row order. The decode is branch-free except for the rare P runs
-// of 3+ users and degree classes outside the LDS table.
-template <int UC>
-__device__ __forceinline__ void accumulate_group(double *acc, const RowIndex *ix, int total,
-                                                 const uint32_t *__restrict__ ent,
-                                                 const double *s_beta, const double *s_inv,
-                                                 const double *__restrict__ g_inv,
-                                                 uint32_t *tr) {
-  const int lane = lane_id();
-  for (int cb = 0; cb < total; cb += 64 * UC) {
-    int rr[UC], cc[UC];
-#pragma unroll
-    for (int q = 0; q < UC; ++q) {
-      const int c = cb + q * 64 + lane;
-      cc[q] = c < total ? c : total - 1;
-      rr[q] = 0;
-    }
-#pragma unroll
-    for (int st = 64; st > 0; st >>= 1)
-#pragma unroll
-      for (int q = 0; q < UC; ++q) rr[q] += ix->cincl[rr[q] + st - 1] <= cc[q] ? st : 0;
-    uint4 w[UC];
-#pragma unroll
-    for (int q = 0; q < UC; ++q)
-      w[q] = *reinterpret_cast<const uint4 *>(ent + ix->base[rr[q]] +
-                                              4 * (cc[q] - ix->cexcl[rr[q]]));
-    // the first two slots after the block (a V value or a P run that straddles it)
-    const int cn = cb + 64 * UC;
-    uint32_t pk0 = 0, pk1 = 0;
-    if (cn < total) {  // wave-uniform
-      int rp = 0;
-#pragma unroll
-      for (int st = 64; st > 0; st >>= 1) rp += ix->cincl[rp + st - 1] <= cn ? st : 0;
-      const uint32_t *p = ent + ix->base[rp] + 4 * (cn - ix->cexcl[rp]);
-      pk0 = p[0];
-      pk1 = p[1];
-    }
-#pragma unroll
-    for (int q = 0; q < UC; ++q) {
-      wave_sync();  // the previous register's readers of tr are done
-      reinterpret_cast<uint4 *>(tr)[lane] = w[q];
-      wave_sync();
-      const uint32_t nx0 = q + 1 < UC ? __builtin_amdgcn_readlane(w[(q + 1 < UC) ? q + 1 : q].x, 0) : pk0;
-      const uint32_t nx1 = q + 1 < UC ? __builtin_amdgcn_readlane(w[(q + 1 < UC) ? q + 1 : q].y, 0) : pk1;
-      // the register's 4 slot-ordered instructions t: every LDS read of the 4 is issued
-      // before any add (the reads then overlap instead of waiting one by one)
-      uint32_t X[4], N1[4], N2[4];
-      int R[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int m = 64 * t + lane;  // slot of this 256-slot register, in order
-        X[t] = tr[m];
-        N1[t] = tr[m + 1 < 256 ? m + 1 : 255];
-        N2[t] = tr[m + 2 < 256 ? m + 2 : 255];
-        R[t] = __shfl(rr[q], m >> 2);
-      }
-      N1[3] = lane == 63 ? nx0 : N1[3];
-      N2[3] = lane == 63 ? nx1 : (lane == 62 ? nx0 : N2[3]);
-      int CX[4], LW[4];
-      double AL[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        CX[t] = ix->cexcl[R[t]];
-        LW[t] = ix->len[R[t]];
-        AL[t] = ix->alpha[R[t]];
-      }
-      bool HEAD[4], ISV[4];
-      int COL[4], SROW[4];
-      uint32_t CI[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int m = 64 * t + lane;
-        const int cabs = cb + q * 64 + (m >> 2);
-        SROW[t] = 4 * (cabs - CX[t]) + (m & 3);  // slot within its row
-        ISV[t] = LW[t] < 0;
-        const bool valid = cabs < total && SROW[t] < (LW[t] & 0x7fffffff);
-        HEAD[t] = valid && (ISV[t] ? (SROW[t] % 3) == 0 : !(X[t] & kIsCont));
-        COL[t] = HEAD[t] ? (int)(X[t] & 0xffffu) : 0;
-        CI[t] = ISV[t] ? 0u : ((X[t] >> 16) & kClsMask);
-      }
-      double NUM[4], BE[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        NUM[t] = s_inv[CI[t] < (uint32_t)kInvTab ? CI[t] : 0u];
-        BE[t] = s_beta[COL[t]];
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bool far = HEAD[t] && !ISV[t] && CI[t] >= (uint32_t)kInvTab;
-        if (__ballot(far))
-          if (far) NUM[t] = g_inv[CI[t]];
-        if (ISV[t]) NUM[t] = __hiloint2double((int)N2[t], (int)N1[t]);  // general_W[i][j]
-        const bool run = HEAD[t] && !ISV[t] && (X[t] & kHasNext);
-        if (__ballot(run)) {  // more users behind this (i, j), ascending v
-          if (run) {
-            NUM[t] += inv_of(N1[t], s_inv, g_inv);
-            if (N1[t] & kHasNext) {
-              NUM[t] += inv_of(N2[t], s_inv, g_inv);
-              if (N2[t] & kHasNext) {  // runs of 4+ (rare): the rest from memory
-                const uint32_t *p = ent + ix->base[R[t]] + SROW[t] + 3;
-                uint32_t y;
-                do {
-                  y = *p++;
-                  NUM[t] += inv_of(y, s_inv, g_inv);
-                } while (y & kHasNext);
-              }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        double den = AL[t] * BE[t];
-        if (den == 0.0) den = 1.0;
-        NUM[t] = NUM[t] / den;
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (HEAD[t])
-          __hip_atomic_fetch_add(&acc[COL[t]], NUM[t], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
+  if (bound[i] > vthr) hub_rows[atomicAdd(n_hub, 1ull)] = i;
 }
 
 template <int Q>
@@ -852,30 +651,39 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
 
 // ------------------------------------------------------------ the tile walk kernel
 // One launch per tile. Persistent waves (NW per workgroup, one workgroup per CU; each wave
-// takes users u, u + G, u + 2G, ... with G = all waves): a user's chain is row pointers ->
-// item ids -> RowMeta -> slots, so while user u's slots are in flight the wave already has
-// the RowMeta of u+G, the item ids of u+2G and the row pointers of u+3G in flight (and, for
-// the top-K mode, u's list, score bounds, embedding and exclusion window).
+// takes users u, u + G, u + 2G, ... with G = all waves). A wave's work is a stream of
+// BATCHES of at most 64 of a user's rows (every user has at least one, possibly empty):
+// lane (g, h) = (lane / 8, lane % 8) loads unit h of row 8q + g for q < 8, so one load
+// instruction moves 8 whole lines. The stream is software-pipelined: while batch t is
+// decoded, the lines and ra of batch t+1 and the item ids of batch t+2 are in flight (and
+// the row pointers of the user after that). Each path is added with one LDS atomic
+// (ds_add_f64); rows whose header says "slow" (V rows, far degree classes) take a general
+// decode, overflow runs are collected in LDS and loaded together after the batch.
 //
-// MODE_F:    F[u][j - item_begin] = the accumulator (lg_spread_tile_resource_f64).
+// MODE_F:    F[u][j - item_begin] = rb_j * acc[j] (lg_spread_tile_resource_f64).
 // MODE_TOPK: the tile's columns of (G *) F merge into the running per-user top-K lists
-//            (lg_spread_tile_resource_topk_f64); F never leaves LDS. With a G factor, a
-//            column's score can only beat the list's K-th value tau if gb * F > tau, gb =
-//            the (user, 64-column chunk) upper bound of the fp32 score chain from
-//            lg_score_chunk_bound (bf16 MFMA + a rigorous rounding margin); only those
-//            columns get the exact chain score. Ids grow along the walk, so "beats" is
-//            v > tau (a tie loses to the older, smaller id).
+//            (lg_spread_tile_resource_topk_f64); F never leaves LDS. A column's score can
+//            only beat the list's K-th value tau if acc * rb_max (* gb) > tau, rb_max = the
+//            tile's largest rb and gb = the (user, 64-column chunk) upper bound of the fp32
+//            score chain from lg_score_chunk_bound (bf16 MFMA + a rigorous rounding margin):
+//            only those columns get rb_j and (with G) the exact chain score. Ids grow along
+//            the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
 constexpr int MODE_F = 0, MODE_TOPK = 1;
+constexpr int kWalkQ = 8;       // line loads per lane per batch: 8 rows each, 64 rows
+constexpr int kBatchRows = 8 * kWalkQ;
+constexpr int kOvfList = kBatchRows;
 
 struct WalkArgs {
   const int64_t *user_rowptr;
   const int32_t *user_items;
+  const double *ra_edge;      // ra of user_items[p], aligned with user_items
   int64_t n_users;
-  const RowMeta *wt_meta;
-  const uint32_t *wt_ent;
+  const uint4 *lines;         // n_items + 1 lines (the last all zero)
+  const uint4 *ovf;
+  int32_t null_row;           // = n_items
   int32_t item_begin, tile, width;
-  const double *beta;   // all items
-  const double *g_inv;  // fl(1/k) per degree class
+  const double *rbeta;  // all items: 1 / beta
+  const double *g_inv;  // fl(1/k) by class number (index 0 unused)
   // MODE_F
   double *F;
   int64_t ldf;
@@ -889,138 +697,342 @@ struct WalkArgs {
   int k, first;
   double *io_val;
   int64_t *io_idx;
+  int dbg;  // measurement knob (LGCNHS_WALK_DBG): 1 = no LDS atomics, 2 = no decode, 4 = no
+            // scan, 16 = plain LDS stores, 32 = atomics to conflict-free addresses
 };
 
+// per wave: acc[tile], the overflow list (decode), the user's embedding and the scoring
+// queue (MODE_TOPK with D > 0; the running list itself lives in registers)
 template <int MODE, int D, int M>
 __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
-  return ((size_t)tile * 8 + sizeof(RowIndex) + 1024 +
-          (MODE == MODE_TOPK ? (size_t)64 * M * 12 + (size_t)(D > 0 ? D : 4) * 4 +
-                                   (D > 0 ? (size_t)128 * 12 : 0)
-                             : 0) + 15) &
+  return ((size_t)tile * 8 + (size_t)kOvfList * 12 +
+          (MODE == MODE_TOPK && D > 0 ? (size_t)D * 4 + (size_t)128 * 12 : 0) + 15) &
          ~(size_t)15;
 }
 __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
-  return (size_t)tile * 8 + (size_t)kInvTab * 8;
+  return (size_t)kInvTab * 8 + 16 * 8;  // class table + the block's rb maxima
 }
 
-template <int MODE, int UF, int D, int M>
+__device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
+  __hip_atomic_fetch_add(&acc[col], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// fl(1/k) of a P slot's degree class (general decode: classes >= kInvTab from memory)
+__device__ __forceinline__ double slot_inv(uint32_t s, const double *s_inv,
+                                           const double *__restrict__ g_inv) {
+  const uint32_t c = s >> 16;
+  const bool far = c >= (uint32_t)kInvTab;
+  const double inv = s_inv[far ? 0u : c];
+  if (__builtin_expect(__ballot(far) != 0, 0)) {  // (a separate load: not a flat select)
+    const double g = __builtin_nontemporal_load(g_inv + (far ? c : 0u));
+    return far ? g : inv;
+  }
+  return inv;
+}
+
+// General decode of one 16-byte unit: a V entry (x has bit 31) or 4 P slots (zero words:
+// padding). head: unit 0 of a line, whose word x is the row header (y, z, w are slots of a
+// P row and zero in a V row).
+__device__ __forceinline__ void add_unit(double *acc, uint4 w, bool head, double ra,
+                                         const double *s_inv, const double *__restrict__ g_inv) {
+  const bool isv = !head && (w.x & kEntV);
+  const uint32_t sx = head ? 0u : w.x;
+  // P slot words only (a V entry's y / z are its value: never decoded as classes)
+  const uint32_t py = isv ? 0u : w.y, pz = isv ? 0u : w.z, pw = isv ? 0u : w.w;
+  const double i0 = slot_inv(isv ? 0u : sx, s_inv, g_inv);
+  const double v0 = (isv ? __hiloint2double((int)w.z, (int)w.y) : i0) * ra;
+  const double v1 = slot_inv(py, s_inv, g_inv) * ra;
+  const double v2 = slot_inv(pz, s_inv, g_inv) * ra;
+  const double v3 = slot_inv(pw, s_inv, g_inv) * ra;
+  if (sx) lds_add(acc, sx & 0xFFFFu, v0);
+  if (py) lds_add(acc, py & 0xFFFFu, v1);
+  if (pz) lds_add(acc, pz & 0xFFFFu, v2);
+  if (pw) lds_add(acc, pw & 0xFFFFu, v3);
+}
+
+// Fast decode (P rows whose classes are all < kInvTab): s_inv sits at LDS address 0.
+__device__ __forceinline__ void add_slot_fast(double *acc, uint32_t s, double ra,
+                                              const double *s_inv) {
+  const double inv = s_inv[s >> 16];
+  if (s) lds_add(acc, s & 0xFFFFu, inv * ra);
+}
+
+// A batch of the wave's stream: rows [r0, r1) of user u (whose rows end at e).
+struct Batch {
+  int64_t u, r0, r1, e;
+  bool first;
+};
+
+template <int MODE, int D, int M>
 __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
-  constexpr int CAP = 64 * M;
+  constexpr int Q = kWalkQ;
   extern __shared__ double lds[];
   const int nw = blockDim.x / 64;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   const int lane = lane_id();
+  const int gh = lane & 7;     // unit of the line this lane loads
+  const int grow = lane >> 3;  // row of the 8-row load group
+  const uint32_t hmask = gh == 0 ? 0u : 0xFFFFFFFFu;  // word x of unit 0 is the header
   const int tile = a.tile;
-  double *s_beta = lds;
-  double *s_inv = s_beta + tile;
-  char *mine = reinterpret_cast<char *>(s_inv + kInvTab) +
+  double *s_inv = lds;  // at LDS address 0 (the fast decode indexes it with class * 8)
+  double *s_red = s_inv + kInvTab;
+  char *mine = reinterpret_cast<char *>(s_red + 16) +
                (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
-  RowIndex *ix = reinterpret_cast<RowIndex *>(acc + tile);
-  uint32_t *tr = reinterpret_cast<uint32_t *>(ix + 1);  // 256-slot transpose scratch
-  double *cs = reinterpret_cast<double *>(tr + 256);
-  int *ci = reinterpret_cast<int *>(cs + CAP);
-  float *us = reinterpret_cast<float *>(ci + CAP);
-  double *pf = reinterpret_cast<double *>(us + (D > 0 ? D : 4));  // candidate queue (D > 0)
+  double *ovl_ra = acc + tile;  // overflow list (decode)
+  uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
+  float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);
+  double *pf = reinterpret_cast<double *>(us + (D > 0 ? D : 0));  // candidate queue (D > 0)
   int *pj = reinterpret_cast<int *>(pf + 128);
-  (void)cs; (void)ci; (void)us; (void)pf; (void)pj;
+  (void)us; (void)pf; (void)pj;
 
-  for (int j = threadIdx.x; j < tile; j += blockDim.x)
-    s_beta[j] = j < a.width ? a.beta[a.item_begin + j] : 0.0;
   for (int c = threadIdx.x; c < kInvTab; c += blockDim.x) s_inv[c] = a.g_inv[c];
+  double rmax = 0.0;  // the tile's largest rb (top-K prefilter)
+  for (int j = threadIdx.x; j < a.width; j += blockDim.x) rmax = fmax(rmax, a.rbeta[a.item_begin + j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, o));
+  if (lane == 0) s_red[wave] = rmax;
   for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
   __syncthreads();
+  rmax = 0.0;
+  for (int w = 0; w < nw; ++w) rmax = fmax(rmax, s_red[w]);
+  // acc * rb_j > tau  implies  acc * rb_max * (1 + 2^-50) > tau (rounding of both products)
+  const double rscale = rmax * (1.0 + 0x1p-50);
 
   const int64_t G = (int64_t)gridDim.x * nw;
-  int64_t u = (int64_t)blockIdx.x * nw + wave;
   const int64_t n_users = a.n_users;
-  if (u >= n_users) return;
+  const int64_t u_first = (int64_t)blockIdx.x * nw + wave;
+  if (u_first >= n_users) return;
 
-  auto rows = [&](int64_t v, int64_t &b, int64_t &e) __attribute__((always_inline)) {
-    b = e = 0;
-    if (v < n_users) {
-      b = a.user_rowptr[v];
-      e = a.user_rowptr[v + 1];
+  // row pointers of the next new user of the stream (prefetched one user ahead)
+  int64_t uq = u_first, bq = a.user_rowptr[u_first], eq = a.user_rowptr[u_first + 1];
+  auto new_user = [&]() __attribute__((always_inline)) {
+    Batch y{uq, bq, bq + kBatchRows < eq ? bq + kBatchRows : eq, eq, true};
+    uq += G;
+    if (uq < n_users) {
+      bq = a.user_rowptr[uq];
+      eq = a.user_rowptr[uq + 1];
+    }
+    return y;
+  };
+  auto next_batch = [&](const Batch &x) __attribute__((always_inline)) {
+    if (x.r1 < x.e) {
+      Batch y{x.u, x.r1, x.r1 + kBatchRows < x.e ? x.r1 + kBatchRows : x.e, x.e, false};
+      return y;
+    }
+    if (x.u + G >= n_users) return Batch{n_users, 0, 0, 0, false};  // end of the stream
+    return new_user();
+  };
+  // item ids of a batch's rows (lanes of one 8-lane group: one row)
+  auto load_ids = [&](const Batch &x, int32_t (&it)[Q]) __attribute__((always_inline)) {
+    if (x.r1 > x.r0) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t r = x.r0 + 8 * q + grow;
+        it[q] = a.user_items[r < x.r1 ? r : x.r0];
+      }
     }
   };
-  auto items = [&](int64_t b, int64_t e, int32_t &i0, int32_t &i1) __attribute__((always_inline)) {
-    i0 = b + lane < e ? a.user_items[b + lane] : -1;
-    i1 = b + 64 + lane < e ? a.user_items[b + 64 + lane] : -1;
-  };
-  auto meta = [&](int32_t i0, int32_t i1, RowMeta &m0, RowMeta &m1) __attribute__((always_inline)) {
-    m0 = i0 >= 0 ? a.wt_meta[i0] : RowMeta{0, 0.0};
-    m1 = i1 >= 0 ? a.wt_meta[i1] : RowMeta{0, 0.0};
+  // lines and ra of a batch (rows past r1 read the zero line)
+  auto load_rows = [&](const Batch &x, const int32_t (&it)[Q], uint4 (&w)[Q], double (&ra)[Q])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t r = x.r0 + 8 * q + grow;
+      const bool in = r < x.r1;
+      w[q] = a.lines[(int64_t)(in ? it[q] : a.null_row) * 8 + gh];
+      ra[q] = a.ra_edge[in ? r : 0];
+    }
   };
 
-  int64_t b0, e0, b1, e1, b2, e2;
-  rows(u, b0, e0);
-  rows(u + G, b1, e1);
-  rows(u + 2 * G, b2, e2);
-  int32_t ia, ib, ja, jb;
-  items(b0, e0, ia, ib);
-  items(b1, e1, ja, jb);
-  RowMeta ma, mb;
-  meta(ia, ib, ma, mb);
-  int64_t xc_next = 0;  // exclusion cursor of the next user (MODE_TOPK)
-  if constexpr (MODE == MODE_TOPK)
-    if (a.ex_rowptr) xc_next = a.ex_cur[u];
-  int total = write_row_index(ix, ma, mb);
-  for (;;) {
-    int32_t ka, kb;
-    items(b2, e2, ka, kb);           // u+2G
-    RowMeta na, nb;
-    meta(ja, jb, na, nb);            // u+G
-    int64_t b3, e3;
-    rows(u + 3 * G, b3, e3);         // u+3G
-    // ---- this user's top-K inputs, in flight beside its slots
-    const int k = a.k;
-    int64_t lid0 = -1, lid1 = -1;
-    double lv0 = 0.0, lv1 = 0.0;
-    float gbv = 0.f, uev0 = 0.f, uev1 = 0.f;
-    int64_t xpos = 0, xhi = 0, xc_after = 0;
-    int32_t xw = 0x7fffffff;
+  // ---- top-K state of the current user (MODE_TOPK), loaded at its first batch
+  constexpr bool kTwo = M > 2;  // k > 64: the list spans two registers per lane
+  int lid0 = -1, lid1 = -1;
+  double lv0 = 0.0, lv1 = 0.0;
+  float gbv = 0.f;
+  int64_t xpos = 0, xhi = 0;
+  int32_t xw = 0x7fffffff;
+  auto load_user = [&](int64_t u) __attribute__((always_inline)) {
     if constexpr (MODE == MODE_TOPK) {
+      const int k = a.k;
+      lid0 = lid1 = -1;
       if (!a.first) {
-        if (lane < k) { lid0 = a.io_idx[u * k + lane]; lv0 = a.io_val[u * k + lane]; }
-        if (64 + lane < k) { lid1 = a.io_idx[u * k + 64 + lane]; lv1 = a.io_val[u * k + 64 + lane]; }
+        // ids < 2^31 (and -1): the low dword of the int64 entry
+        const int *idx32 = reinterpret_cast<const int *>(a.io_idx);
+        const int e0 = lane < k ? lane : k - 1;
+        lid0 = idx32[2 * (u * k + e0)];
+        lv0 = a.io_val[u * k + e0];
+        if (lane >= k) lid0 = -1;
+        if constexpr (kTwo) {
+          const int e1 = 64 + lane < k ? 64 + lane : k - 1;
+          lid1 = idx32[2 * (u * k + e1)];
+          lv1 = a.io_val[u * k + e1];
+          if (64 + lane >= k) lid1 = -1;
+        }
       }
-      if constexpr (D > 0) {
-        if (lane < a.nch) gbv = a.gb[u * a.nch + lane];
-        if (lane < D) uev0 = a.eu[u * D + lane];
-        if (D > 64 && 64 + lane < D) uev1 = a.eu[u * D + 64 + lane];
-      }
+      if constexpr (D > 0) gbv = a.gb[u * a.nch + (lane < a.nch ? lane : 0)];
       if (a.ex_rowptr) {
-        xpos = xc_next;
+        xpos = a.ex_cur[u];
         xhi = a.ex_rowptr[u + 1];
-        if (u + G < n_users) xc_after = a.ex_cur[u + G];
+        xw = 0x7fffffff;
         if (xpos + lane < xhi) xw = a.ex_col[xpos + lane];
       }
     }
-    accumulate_group<UF>(acc, ix, total, a.wt_ent, s_beta, s_inv, a.g_inv, tr);
-    for (int64_t p0 = b0 + kResRows; p0 < e0; p0 += kResRows) {  // rows beyond 128 items
-      int32_t xa, xb;
-      items(p0, e0, xa, xb);
-      RowMeta ya, yb;
-      meta(xa, xb, ya, yb);
-      const int t2 = write_row_index(ix, ya, yb);
-      accumulate_group<UF>(acc, ix, t2, a.wt_ent, s_beta, s_inv, a.g_inv, tr);
+  };
+
+  // ---- decode one batch into acc
+  double dbg_sink = 0.0;
+  auto decode = [&](const Batch &x, uint4 (&w)[Q], const double (&ra)[Q])
+      __attribute__((always_inline)) {
+    if (a.dbg & 2) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) dbg_sink += (double)(w[q].x ^ w[q].y ^ w[q].z ^ w[q].w) * ra[q];
+      return;
     }
+    if (a.dbg & 1) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint32_t s0 = w[q].x & hmask;
+        dbg_sink += s_inv[s0 >> 16] * ra[q] + s_inv[w[q].y >> 16] * ra[q] +
+                    s_inv[w[q].z >> 16] * ra[q] + s_inv[w[q].w >> 16] * ra[q];
+      }
+      return;
+    }
+    if (a.dbg & 48) {  // 16: plain stores instead of atomics; 32: atomics to acc[lane]
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint32_t sv[4] = {w[q].x & hmask, w[q].y, w[q].z, w[q].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const double v = s_inv[sv[t] >> 16] * ra[q];
+          if (sv[t]) {
+            if (a.dbg & 16) acc[sv[t] & 0xFFFFu] = v;
+            else lds_add(acc, (uint32_t)(lane * 4 + t), v);
+          }
+        }
+      }
+      return;
+    }
+    uint32_t hdr = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) hdr |= w[q].x & ~hmask;  // the group heads' headers
+    const bool slow = __ballot(hdr & kHdrSlow) != 0;
+    const bool ovf = __ballot(hdr & kHdrOvf) != 0;
+    if (!slow) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        add_slot_fast(acc, w[q].x & hmask, ra[q], s_inv);
+        add_slot_fast(acc, w[q].y, ra[q], s_inv);
+        add_slot_fast(acc, w[q].z, ra[q], s_inv);
+        add_slot_fast(acc, w[q].w, ra[q], s_inv);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) add_unit(acc, w[q], gh == 0, ra[q], s_inv, a.g_inv);
+    }
+    if (ovf) {  // overflow runs: collected, then up to 4 rows' first 64 units in flight
+      int nov = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const bool o = gh == 0 && (w[q].x & kHdrOvf);
+        const uint64_t bal = __ballot(o);
+        if (o) {
+          const int p = nov + __popcll(bal & lanemask_lt());
+          ovl_ent[p] = w[q].x & kHdrPtr;
+          ovl_ra[p] = ra[q];
+        }
+        nov += __popcll(bal);
+      }
+      wave_sync();
+      for (int t0 = 0; t0 < nov; t0 += 4) {
+        uint4 y4[4];
+        uint32_t ou4[4];
+        double r4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool in = t0 + j < nov;
+          ou4[j] = ovl_ent[in ? t0 + j : t0];
+          r4[j] = ovl_ra[in ? t0 + j : t0];
+          y4[j] = a.ovf[(int64_t)ou4[j] + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (t0 + j >= nov) continue;
+          const uint32_t n = (uint32_t)__shfl((int)y4[j].x, 0);
+          if (lane == 0 || (uint32_t)lane > n) y4[j] = uint4{0u, 0u, 0u, 0u};
+          add_unit(acc, y4[j], false, r4[j], s_inv, a.g_inv);
+          for (uint32_t c = 64; c <= n; c += 64) {  // runs longer than 63 units
+            const uint32_t cc = c + lane;
+            const uint4 y = cc <= n ? a.ovf[(int64_t)ou4[j] + cc] : uint4{0u, 0u, 0u, 0u};
+            add_unit(acc, y, false, r4[j], s_inv, a.g_inv);
+          }
+        }
+      }
+      wave_sync();
+    }
+  };
+
+  // ---- the user's tile of F: written out (MODE_F) or merged into its top-K list
+  auto finish_user = [&](int64_t u) __attribute__((always_inline)) {
     wave_sync();
+    if (a.dbg & 4) {
+      if (dbg_sink == 1.2345) acc[lane] = dbg_sink;  // keeps the debug sums alive
+      return;
+    }
     if constexpr (MODE == MODE_F) {
       double *row = a.F + u * a.ldf;
       for (int j = lane; j < tile; j += 64) {
-        __builtin_nontemporal_store(acc[j], row + j);
+        const double rb = j < a.width ? a.rbeta[a.item_begin + (j < a.width ? j : 0)] : 0.0;
+        __builtin_nontemporal_store(acc[j] * rb, row + j);
         acc[j] = 0.0;
       }
     } else {
-      // running list -> LDS (valid entries form a sorted prefix)
-      int cnt = __popcll(__ballot(lid0 >= 0)) + __popcll(__ballot(lid1 >= 0));
-      if (lid0 >= 0) { cs[lane] = lv0; ci[lane] = (int)lid0; }
-      if (lid1 >= 0) { cs[64 + lane] = lv1; ci[64 + lane] = (int)lid1; }
-      if constexpr (D > 0) {
-        if (lane < D) us[lane] = uev0;
-        if (D > 64 && 64 + lane < D) us[64 + lane] = uev1;
-      }
+      const int k = a.k;
+      // the running list in registers: entry lane (L0, I0) and 64 + lane (L1, I1), sorted by
+      // (value desc, id asc); empty entries (-inf, kPadId)
+      double L0 = lid0 >= 0 ? lv0 : neg_inf<double>();
+      double L1 = kTwo && lid1 >= 0 ? lv1 : neg_inf<double>();
+      int I0 = lid0 >= 0 ? lid0 : kPadId;
+      int I1 = kTwo && lid1 >= 0 ? lid1 : kPadId;
+      auto kth = [&](double &tv, int &ti) __attribute__((always_inline)) {
+        if (!kTwo || k <= 64) {
+          tv = __shfl(L0, k - 1);
+          ti = __shfl(I0, k - 1);
+        } else {
+          tv = __shfl(L1, k - 65);
+          ti = __shfl(I1, k - 65);
+        }
+      };
+      double tau;
+      int tau_id;
+      kth(tau, tau_id);
+      bool dirty = a.first != 0;
+      // insert (v, id) (wave-uniform) if it beats the k-th entry: its rank is the number of
+      // entries before it; the entries from that rank on move one place down
+      auto insert1 = [&](double v, int id) __attribute__((always_inline)) {
+        if (!before(v, id, tau, tau_id)) return;
+        dirty = true;
+        int pos = __popcll(__ballot(before(L0, I0, v, id)));
+        if constexpr (kTwo) pos += __popcll(__ballot(before(L1, I1, v, id)));
+        const double up0 = __shfl_up(L0, 1);
+        const int iu0 = __shfl_up(I0, 1);
+        if constexpr (kTwo) {
+          const double up1 = __shfl_up(L1, 1);
+          const int iu1 = __shfl_up(I1, 1);
+          const double c0 = __shfl(L0, 63);
+          const int ic0 = __shfl(I0, 63);
+          const int p1 = 64 + lane;
+          const double n1 = p1 > pos ? (lane == 0 ? c0 : up1) : (p1 == pos ? v : L1);
+          const int m1 = p1 > pos ? (lane == 0 ? ic0 : iu1) : (p1 == pos ? id : I1);
+          L1 = p1 < k ? n1 : neg_inf<double>();
+          I1 = p1 < k ? m1 : kPadId;
+        }
+        L0 = lane > pos ? up0 : (lane == pos ? v : L0);
+        I0 = lane > pos ? iu0 : (lane == pos ? id : I0);
+        if (lane >= k) { L0 = neg_inf<double>(); I0 = kPadId; }
+        kth(tau, tau_id);
+      };
+      bool us_ready = false;  // the user's embedding row is copied to LDS at the first flush
       // excluded items of this tile (the next run of the user's sorted exclusion row): -1
       const int32_t lim = a.item_begin + a.width;
       if (a.ex_rowptr) {
@@ -1035,31 +1047,24 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         if (lane == 0) a.ex_cur[u] = xpos;
       }
       wave_sync();
-      double tau = neg_inf<double>();
-      int tau_id = kPadId;
-      if (cnt == k) { tau = cs[k - 1]; tau_id = ci[k - 1]; }
-      bool dirty = a.first != 0;
-      // insert the lanes' (v, item) with cand set; compact when the list could overflow
-      auto insert = [&](bool cand, double v, int item) __attribute__((always_inline)) {
-        const uint64_t bal = __ballot(cand);
-        if (!bal) return;
-        dirty = true;
-        const int p = cnt + __popcll(bal & lanemask_lt());
-        if (cand) {
-          cs[p] = v;
-          ci[p] = item;
-        }
-        cnt += __popcll(bal);
-        if (cnt > CAP - 64) {
-          wave_sync();
-          cnt = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
-        }
-      };
-      if constexpr (D > 0) {
-        // columns whose bound gb * F beats tau are queued (pj/pf, ascending), and scored
-        // 64 at a time, one lane each: one round of item-row loads per 64 candidates
-        int np = 0;
-        auto flush = [&](int m) __attribute__((always_inline)) {
+      // The scan: lane l reads columns c0 + 2l, c0 + 2l + 1 (ds_read_b128), 4 reads in flight
+      // (512 columns). A column can enter only if acc > thr, thr = tau / (rb_max (1 + 2^-50)
+      // [* max(gb, 0)]) (>= -0.5: excluded columns hold -1; every rounding of
+      // fl(gb fl(acc rb_j)) > tau is covered by the 2^-50 margin); those get rb_j and (with G)
+      // the exact score. The list order (value desc, id asc) is total, so the order in which
+      // candidates are inserted does not matter.
+      int np = 0;  // scoring queue (D > 0)
+      auto flush = [&](int m) __attribute__((always_inline)) {
+        if constexpr (D > 0) {
+          if (!us_ready) {
+            const float e0 = a.eu[u * D + (lane < D ? lane : 0)];
+            if (lane < D) us[lane] = e0;
+            if constexpr (D > 64) {
+              const float e1 = a.eu[u * D + (64 + lane < D ? 64 + lane : 0)];
+              if (64 + lane < D) us[64 + lane] = e1;
+            }
+            us_ready = true;
+          }
           wave_sync();
           bool cand = lane < m;
           double v = 0.0;
@@ -1067,21 +1072,26 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           if (cand) {
             item = a.item_begin + pj[lane];
             v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * pf[lane];
-            cand = v > tau;
           }
           wave_sync();
           if (np > 64) {  // keep the queue's tail
             if (lane < np - 64) { pj[lane] = pj[64 + lane]; pf[lane] = pf[64 + lane]; }
           }
           np = np > 64 ? np - 64 : 0;
-          insert(cand, v, item);
-        };
-        for (int c0 = 0; c0 < a.width; c0 += 64) {
-          const int j = c0 + lane;
-          const double f = j < a.width ? acc[j] : -1.0;
-          if (j < tile) acc[j] = 0.0;
-          const float gbc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gbv), c0 >> 6));
-          const bool cand = f >= 0.0 && (double)gbc * f > tau;
+          uint64_t bal = __ballot(cand && before(v, item, tau, tau_id));
+          while (bal) {
+            const int l = __ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+            insert1(__shfl(v, l), __shfl(item, l));
+          }
+        }
+      };
+      // one column of a lane that passed the prefilter (pre: lanes with a candidate)
+      auto take = [&](bool pre, double sacc, int j, float gbc) __attribute__((always_inline)) {
+        if (!__ballot(pre)) return;
+        const double f = pre ? sacc * a.rbeta[a.item_begin + (pre ? j : 0)] : -1.0;
+        if constexpr (D > 0) {
+          const bool cand = pre && (double)gbc * f > tau;
           const uint64_t bal = __ballot(cand);
           if (bal) {
             const int p = np + __popcll(bal & lanemask_lt());
@@ -1092,35 +1102,111 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             np += __popcll(bal);
             if (np >= 64) flush(64);
           }
+        } else {
+          uint64_t bal = __ballot(pre && before(f, a.item_begin + j, tau, tau_id));
+          while (bal) {
+            const int l = __ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+            insert1(__shfl(f, l), a.item_begin + __shfl(j, l));
+          }
         }
-        while (np > 0) flush(np < 64 ? np : 64);
-      } else {
-        for (int c0 = 0; c0 < a.width; c0 += 64) {
-          const int j = c0 + lane;
-          const double f = j < a.width ? acc[j] : -1.0;
-          if (j < tile) acc[j] = 0.0;
-          insert(f >= 0.0 && f > tau, f, a.item_begin + j);
+      };
+      // thresholds: no G, one per user (thr_s); with G, one per 64-column chunk c in lane c
+      // (thr_v); refreshed when tau moves
+      double thr_s = 0.0, thr_v = 0.0;
+      double tau_seen = 0.0;
+      auto refresh = [&]() __attribute__((always_inline)) {
+        if constexpr (D > 0) {
+          const double bnd = rscale * (double)fmaxf(gbv, 0.f);
+          const double t = tau / bnd;
+          thr_v = t > -0.5 ? t : -0.5;
+        } else {
+          const double t = tau / rscale;
+          thr_s = t > -0.5 ? t : -0.5;
+        }
+        tau_seen = tau;
+      };
+      refresh();
+      const double2 zero2{0.0, 0.0};
+      for (int c0 = 0; c0 < a.width; c0 += 512) {
+        double2 s4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = c0 + 128 * t + 2 * lane;
+          s4[t] = j < tile ? *reinterpret_cast<const double2 *>(acc + j) : double2{-1.0, -1.0};
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = c0 + 128 * t + 2 * lane;
+          if (j < tile) *reinterpret_cast<double2 *>(acc + j) = zero2;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = c0 + 128 * t + 2 * lane;
+          float gbc = 0.f;
+          double thr = thr_s;
+          if constexpr (D > 0) {
+            gbc = __shfl(gbv, (j >> 6) & 63);
+            thr = __shfl(thr_v, (j >> 6) & 63);
+          }
+          const double sx = j < a.width ? s4[t].x : -1.0;
+          const double sy = j + 1 < a.width ? s4[t].y : -1.0;
+          if (__ballot(sx > thr || sy > thr)) {
+            take(sx > thr, sx, j, gbc);
+            if (tau != tau_seen) refresh();
+            if constexpr (D > 0) thr = __shfl(thr_v, (j >> 6) & 63);
+            else thr = thr_s;
+            take(sy > thr, sy, j + 1, gbc);
+            if (tau != tau_seen) refresh();
+          }
         }
       }
+      while (np > 0) flush(np < 64 ? np : 64);
+      for (int j = a.width + lane; j < tile; j += 64) acc[j] = 0.0;  // (never touched)
       if (dirty) {
-        wave_sync();
-        const int nc = wave_compact<double, M>(cs, ci, cnt, k, tau, tau_id);
-        for (int e = lane; e < k; e += 64) {
-          a.io_val[u * k + e] = e < nc ? cs[e] : neg_inf<double>();
-          a.io_idx[u * k + e] = e < nc ? ci[e] : -1;
+        if (lane < k) {
+          a.io_val[u * k + lane] = I0 != kPadId ? L0 : neg_inf<double>();
+          a.io_idx[u * k + lane] = I0 != kPadId ? I0 : -1;
+        }
+        if (kTwo && 64 + lane < k) {
+          a.io_val[u * k + 64 + lane] = I1 != kPadId ? L1 : neg_inf<double>();
+          a.io_idx[u * k + 64 + lane] = I1 != kPadId ? I1 : -1;
         }
       }
       wave_sync();
-      xc_next = xc_after;
     }
-    const bool more = u + G < n_users;
-    if (!more) break;
-    total = write_row_index(ix, na, nb);
-    u += G;
-    b0 = b1; e0 = e1;
-    b1 = b2; e1 = e2;
-    b2 = b3; e2 = e3;
-    ja = ka; jb = kb;
+  };
+
+  // ---- the pipeline: c (decoded now; lines in wc), d (lines in flight in wd), n2 (ids in
+  // flight in it2). Two register sets alternate between c and d.
+  int32_t it2[Q];
+  uint4 w0[Q], w1[Q];
+  double ra0[Q], ra1[Q];
+  Batch c = new_user();
+  load_ids(c, it2);
+  load_rows(c, it2, w0, ra0);
+  Batch d = next_batch(c);
+  if (d.u < n_users) {
+    load_ids(d, it2);
+    load_rows(d, it2, w1, ra1);
+  }
+  Batch n2 = d.u < n_users ? next_batch(d) : Batch{n_users, 0, 0, 0, false};
+  if (n2.u < n_users) load_ids(n2, it2);
+  auto step = [&](uint4 (&wc)[Q], double (&rc)[Q]) __attribute__((always_inline)) {
+    if (c.first) load_user(c.u);
+    decode(c, wc, rc);
+    if (c.r1 >= c.e) finish_user(c.u);
+    if (n2.u < n_users) load_rows(n2, it2, wc, rc);  // batch t+2 into the freed registers
+    const Batch n3 = n2.u < n_users ? next_batch(n2) : Batch{n_users, 0, 0, 0, false};
+    if (n3.u < n_users) load_ids(n3, it2);
+    c = d;
+    d = n2;
+    n2 = n3;
+    return c.u < n_users;
+  };
+  for (;;) {
+    if (!step(w0, ra0)) break;
+    if (!step(w1, ra1)) break;
   }
 }
 
@@ -1278,6 +1364,15 @@ extern "C" int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, doub
   return launch_status("lg_hybrid_factors_f64");
 }
 
+extern "C" int lg_hybrid_recip_f64(const double *k_item, int64_t n_items, double lambda,
+                                   double *ra, double *rb, lg_stream_t stream) {
+  LG_REQUIRE(k_item && ra && rb && n_items >= 0, "lg_hybrid_recip_f64: bad arguments");
+  if (n_items == 0) return LG_OK;
+  k_hybrid_recip<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0,
+                   (hipStream_t)stream>>>(k_item, n_items, lambda, ra, rb);
+  return launch_status("lg_hybrid_recip_f64");
+}
+
 extern "C" int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *inv,
                                  lg_stream_t stream) {
   LG_REQUIRE(rowptr && inv && n_rows >= 0, "lg_inv_degree_f64: bad arguments");
@@ -1310,46 +1405,54 @@ extern "C" int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *i
   return launch_status("lg_spread_tile_bound");
 }
 
-extern "C" size_t lg_spread_tile_weight_ws_bytes(int64_t n_items) {
+extern "C" size_t lg_spread_tile_rows_ws_bytes(int64_t n_items) {
   return (size_t)(n_items + 1) * sizeof(int64_t);  // hub count + hub row list
 }
 
-extern "C" int lg_spread_tile_weight_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                                         const int32_t *user_items, const uint16_t *user_cls,
-                                         const double *inv_deg, int64_t n_items,
-                                         const int64_t *cur, const uint16_t *count,
-                                         const double *alpha, const double *beta,
-                                         int32_t item_begin, int32_t tile, const int64_t *bound,
-                                         const int64_t *wt_ptr, void *wt_ent, void *wt_meta,
-                                         void *ws, size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && count && alpha && beta && bound &&
-                 wt_ptr && wt_ent && wt_meta && n_items >= 0,
-             "lg_spread_tile_weight_f64: bad arguments");
+extern "C" int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                                       const int32_t *user_items, const uint16_t *user_cls,
+                                       const double *inv_deg, int64_t n_items,
+                                       const int64_t *cur, const uint16_t *count,
+                                       int32_t item_begin, int32_t tile, const int64_t *bound,
+                                       int64_t vthr, const int64_t *ovf_ptr, void *lines,
+                                       void *ovf, int32_t *row_len, void *ws, size_t ws_bytes,
+                                       lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && count && bound && ovf_ptr && lines &&
+                 ovf && n_items >= 0 && vthr >= kLineSlots,
+             "lg_spread_tile_rows_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && item_begin >= 0,
-             "lg_spread_tile_weight_f64: tile %d not in [1, 8192]", tile);
+             "lg_spread_tile_rows_f64: tile %d not in [1, 8192]", tile);
   if (n_items == 0) return LG_OK;
-  const size_t need = lg_spread_tile_weight_ws_bytes(n_items);
+  const size_t need = lg_spread_tile_rows_ws_bytes(n_items);
   if (!ws || ws_bytes < need) {
-    set_error("lg_spread_tile_weight_f64: workspace %zu < %zu bytes", ws_bytes, need);
+    set_error("lg_spread_tile_rows_f64: workspace %zu < %zu bytes", ws_bytes, need);
     return LG_ERR_WORKSPACE;
   }
   hipStream_t s = (hipStream_t)stream;
   int64_t *n_hub = (int64_t *)ws;
   int64_t *hub_rows = n_hub + 1;
   if (hipMemsetAsync(n_hub, 0, sizeof(int64_t), s) != hipSuccess) {
-    set_error("lg_spread_tile_weight_f64: hipMemsetAsync failed");
+    set_error("lg_spread_tile_rows_f64: hipMemsetAsync failed");
     return LG_ERR_HIP;
   }
-  const unsigned rb = (unsigned)((n_items + 3) / 4);
-  k_tile_weight<<<dim3(rb), dim3(256), 0, s>>>(item_rowptr, item_users, user_items, user_cls,
-                                               n_items, cur, count, alpha, item_begin, bound,
-                                               wt_ptr, (uint32_t *)wt_ent, (RowMeta *)wt_meta);
+  k_tile_rows<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, s>>>(
+      item_rowptr, item_users, user_items, user_cls, n_items, cur, count, item_begin, bound, vthr,
+      ovf_ptr, (uint32_t *)lines, (uint32_t *)ovf, row_len);
   k_hub_list<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
-      bound, n_items, (unsigned long long *)n_hub, hub_rows);
-  k_tile_weight_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
-      hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, alpha, beta,
-      item_begin, tile, wt_ptr, (uint32_t *)wt_ent, (RowMeta *)wt_meta);
-  return launch_status("lg_spread_tile_weight_f64");
+      bound, n_items, vthr, (unsigned long long *)n_hub, hub_rows);
+  k_tile_rows_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
+      hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, item_begin, tile,
+      ovf_ptr, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+  return launch_status("lg_spread_tile_rows_f64");
+}
+
+static int walk_dbg() {  // measurement knob only: results are wrong when set
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("LGCNHS_WALK_DBG");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 static int n_cus() {
@@ -1366,7 +1469,7 @@ static int n_cus() {
 
 // waves per workgroup: as many as the LDS holds next to the shared tables (<= 8), one
 // workgroup per CU, persistent
-template <int MODE, int UF, int D, int M>
+template <int MODE, int D, int M>
 static int launch_walk(const WalkArgs &a, hipStream_t s) {
   const size_t per = walk_wave_bytes<MODE, D, M>(a.tile);
   const size_t shared = walk_shared_bytes(a.tile);
@@ -1381,17 +1484,19 @@ static int launch_walk(const WalkArgs &a, hipStream_t s) {
   const int64_t cap = n_cus();
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   const size_t lds = shared + (size_t)nw * per;
-  k_tile_walk<MODE, UF, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
+  k_tile_walk<MODE, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
   return LG_OK;
 }
 
 extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
-                                           const int32_t *user_items, int64_t n_users,
-                                           const void *wt_meta, const void *wt_ent,
-                                           const double *beta, const double *inv_cls,
+                                           const int32_t *user_items, const double *ra_edge,
+                                           int64_t n_users, const void *lines, const void *ovf,
+                                           int32_t null_row,
+                                           const double *rbeta, const double *inv_cls,
                                            int32_t item_begin, int32_t tile, int32_t width,
                                            double *F, int64_t ldf, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && wt_meta && beta && inv_cls && F && n_users >= 0 && ldf >= tile,
+  LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls && F &&
+                 n_users >= 0 && ldf >= tile,
              "lg_spread_tile_resource_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile,
              "lg_spread_tile_resource_f64: tile %d / width %d", tile, width);
@@ -1399,17 +1504,20 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
   WalkArgs a{};
   a.user_rowptr = user_rowptr;
   a.user_items = user_items;
+  a.ra_edge = ra_edge;
   a.n_users = n_users;
-  a.wt_meta = (const RowMeta *)wt_meta;
-  a.wt_ent = (const uint32_t *)wt_ent;
+  a.lines = (const uint4 *)lines;
+  a.ovf = (const uint4 *)ovf;
+  a.null_row = null_row;
   a.item_begin = item_begin;
   a.tile = tile;
   a.width = width;
-  a.beta = beta;
+  a.rbeta = rbeta;
   a.g_inv = inv_cls;
   a.F = F;
   a.ldf = ldf;
-  const int st = launch_walk<MODE_F, 4, 0, 1>(a, (hipStream_t)stream);
+  a.dbg = walk_dbg();
+  const int st = launch_walk<MODE_F, 0, 1>(a, (hipStream_t)stream);
   if (st != LG_OK) return st;
   return launch_status("lg_spread_tile_resource_f64");
 }
@@ -1456,26 +1564,18 @@ extern "C" size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k
 
 template <int D>
 static int launch_fused(int M, const WalkArgs &a, hipStream_t s) {
-  // LGCNHS_WALK_UC (A/B knob): 4-slot chunk registers per block (2 or 8; default 4)
-  static int uc = -1;
-  if (uc < 0) {
-    const char *e = getenv("LGCNHS_WALK_UC");
-    uc = e ? atoi(e) : 4;
-  }
-  if (M == 2 && uc == 2) return launch_walk<MODE_TOPK, 2, D, 2>(a, s);
-  if (M == 2 && uc == 8) return launch_walk<MODE_TOPK, 8, D, 2>(a, s);
-  return M == 2 ? launch_walk<MODE_TOPK, 4, D, 2>(a, s) : launch_walk<MODE_TOPK, 4, D, 4>(a, s);
+  return M == 2 ? launch_walk<MODE_TOPK, D, 2>(a, s) : launch_walk<MODE_TOPK, D, 4>(a, s);
 }
 
 extern "C" int lg_spread_tile_resource_topk_f64(
-    const int64_t *user_rowptr, const int32_t *user_items, int64_t n_users,
-    const void *wt_meta, const void *wt_ent, const double *beta, const double *inv_cls,
-    int32_t item_begin, int32_t tile, int32_t width, const float *eu, const float *ei,
-    int32_t dim, const float *gb, int32_t n_chunks, const int64_t *ex_rowptr,
+    const int64_t *user_rowptr, const int32_t *user_items, const double *ra_edge,
+    int64_t n_users, const void *lines, const void *ovf, int32_t null_row, const double *rbeta,
+    const double *inv_cls, int32_t item_begin, int32_t tile, int32_t width, const float *eu,
+    const float *ei, int32_t dim, const float *gb, int32_t n_chunks, const int64_t *ex_rowptr,
     const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
     int64_t *io_idx, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && wt_meta && beta && inv_cls && io_val && io_idx && n_users >= 0 &&
-                 item_begin >= 0,
+  LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls &&
+                 io_val && io_idx && n_users >= 0 && item_begin >= 0,
              "lg_spread_tile_resource_topk_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile &&
                  (int64_t)item_begin + width < 0x7fffffff,
@@ -1487,19 +1587,24 @@ extern "C" int lg_spread_tile_resource_topk_f64(
              "lg_spread_tile_resource_topk_f64: dim %d not in {32,64,128}", dim);
   LG_REQUIRE(!eu || n_chunks == (width + 63) / 64,
              "lg_spread_tile_resource_topk_f64: n_chunks %d != ceil(width / 64)", n_chunks);
+  LG_REQUIRE(!eu || n_chunks <= 64,
+             "lg_spread_tile_resource_topk_f64: a G factor needs width <= 4096 (one chunk "
+             "bound per lane), got %d", width);
   LG_REQUIRE(!ex_rowptr == !ex_col && !ex_rowptr == !ex_cur,
              "lg_spread_tile_resource_topk_f64: ex_rowptr/ex_col/ex_cur go together");
   if (n_users == 0) return LG_OK;
   WalkArgs a{};
   a.user_rowptr = user_rowptr;
   a.user_items = user_items;
+  a.ra_edge = ra_edge;
   a.n_users = n_users;
-  a.wt_meta = (const RowMeta *)wt_meta;
-  a.wt_ent = (const uint32_t *)wt_ent;
+  a.lines = (const uint4 *)lines;
+  a.ovf = (const uint4 *)ovf;
+  a.null_row = null_row;
   a.item_begin = item_begin;
   a.tile = tile;
   a.width = width;
-  a.beta = beta;
+  a.rbeta = rbeta;
   a.g_inv = inv_cls;
   a.eu = eu;
   a.ei = ei;
@@ -1512,6 +1617,7 @@ extern "C" int lg_spread_tile_resource_topk_f64(
   a.first = first;
   a.io_val = io_val;
   a.io_idx = io_idx;
+  a.dbg = walk_dbg();
   hipStream_t s = (hipStream_t)stream;
   const int M = k <= 64 ? 2 : 4;
   int st;

@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "liblgcnhs.so")
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -69,18 +69,19 @@ SIGNATURES = {
         [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
     ),
     "lg_hybrid_factors_f64": (ctypes.c_int, [_vp, _i64, _f64, _vp, _vp, _vp]),
+    "lg_hybrid_recip_f64": (ctypes.c_int, [_vp, _i64, _f64, _vp, _vp, _vp]),
     "lg_inv_degree_f64": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
     "lg_spread_tile_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "lg_spread_tile_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
-    "lg_spread_tile_weight_ws_bytes": (_sz, [_i64]),
-    "lg_spread_tile_weight_f64": (
+    "lg_spread_tile_rows_ws_bytes": (_sz, [_i64]),
+    "lg_spread_tile_rows_f64": (
         ctypes.c_int,
-        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
+        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp,
          _vp, _sz, _vp],
     ),
     "lg_spread_tile_resource_f64": (
         ctypes.c_int,
-        [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
+        [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
     ),
     "lg_tile_topk_f64": (
         ctypes.c_int,
@@ -91,8 +92,8 @@ SIGNATURES = {
     "lg_spread_tile_resource_topk_lds_bytes": (_sz, [_i32, _i32, _i32]),
     "lg_spread_tile_resource_topk_f64": (
         ctypes.c_int,
-        [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32,
-         _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+        [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp,
+         _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "lg_bound_prep_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "lg_score_chunk_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp,
                                             _vp]),

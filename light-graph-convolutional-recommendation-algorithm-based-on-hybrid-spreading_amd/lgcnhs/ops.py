@@ -344,15 +344,40 @@ def hybrid_factors(k_item: torch.Tensor, lam: float):
     return alpha, beta
 
 
-SORT_MAX = 256     # pairs per row of the in-wave sort: longer rows are hub (V) rows
 INV_TAB = 512      # degree classes cached in LDS by the walk (csrc/spread_tiled.hip)
-MAX_CLASSES = 0x3FFF
+MAX_CLASSES = 0x7FFF   # P slot words keep bit 31 clear (it marks V entries)
+LINE_SLOTS, LINE_ENTS = 31, 7   # P slots / V entries in a row's 128-byte line
+
+
+def hybrid_recip(k_item: torch.Tensor, lam: float):
+    """(ra, rb) = (1 / k_i^(1-lambda), 1 / k_i^lambda), a zero factor -> 1: the walk's
+    HybridS factors (lg_hybrid_recip_f64)."""
+    k_item = k_item.contiguous().to(torch.float64)
+    n = k_item.shape[0]
+    ra = torch.empty(n, dtype=torch.float64, device=k_item.device)
+    rb = torch.empty_like(ra)
+    N.check(N.lib().lg_hybrid_recip_f64(N.ptr(k_item), n, float(lam), N.ptr(ra), N.ptr(rb),
+                                        N.stream_handle(k_item.device)), "lg_hybrid_recip_f64")
+    return ra, rb
+
+
+class HybridScale:
+    """The lambda-dependent side of the factored spreading: rb = 1/beta per item and
+    ra_edge = 1/alpha of the item of every interaction, aligned with A.by_user.col (so the
+    walk reads a user's factors contiguously with its item ids)."""
+
+    def __init__(self, A: "Interactions", lam: float):
+        self.lam = float(lam)
+        ra, self.rb = hybrid_recip(A.k_item, lam)
+        # one entry past the interactions: the walk's padding rows read it (never used)
+        self.ra_edge = torch.cat([ra[A.by_user.col.to(torch.int64)], ra.new_zeros(1)])
 
 
 def degree_classes(deg: torch.Tensor):
-    """(class of each row's degree as uint16, fp64 fl(1/k) per class): the P-row slot code
-    of csrc/spread_tiled.hip. Classes are ordered by how many rows have the degree, so the
-    common ones fall in the walk's LDS table. Rows of degree 0 get class 0 (never used)."""
+    """(1-based class of each row's degree as uint16, fp64 table inv[c] = fl(1/k) of class
+    c, inv[0] = 0): the slot code of the P rows of csrc/spread_tiled.hip. Classes are
+    numbered by how many rows have the degree, so the common ones fall in the walk's LDS
+    table (c < 512). Rows of degree 0 get class 0 (they are in no pair)."""
     dev = deg.device
     pos = deg[deg > 0]
     if pos.numel() == 0:
@@ -367,25 +392,38 @@ def degree_classes(deg: torch.Tensor):
     rank[order] = torch.arange(order.numel(), device=dev)
     cls = torch.zeros(deg.numel(), dtype=torch.int32, device=dev)
     m = deg > 0
-    cls[m] = rank[torch.searchsorted(uniq, deg[m])].to(torch.int32)
-    inv = torch.zeros(max(INV_TAB, uniq.numel()), dtype=torch.float64, device=dev)
-    inv[:uniq.numel()] = 1.0 / uniq[order].to(torch.float64)
+    cls[m] = (rank[torch.searchsorted(uniq, deg[m])] + 1).to(torch.int32)
+    inv = torch.zeros(max(INV_TAB, uniq.numel() + 1), dtype=torch.float64, device=dev)
+    inv[1:uniq.numel() + 1] = 1.0 / uniq[order].to(torch.float64)
     return cls.to(torch.int16).view(torch.uint16), inv
 
 
-class TileWeights:
-    """W = HybridS(general_W) restricted to one item tile, row-major over all items
-    (lg_spread_tile_* of include/lgcnhs.h; P rows = the (user, item) pairs as 4-byte slots,
-    V rows = merged fp64 values of hub items). ``advance()`` moves to the next tile; the
-    buffers are reused and grown on demand."""
+def _run_units(length: torch.Tensor, hub: torch.Tensor) -> torch.Tensor:
+    """Overflow units (run header + data) of rows with `length` pairs (P) / entries (V)."""
+    p = torch.where(length > LINE_SLOTS, 1 + (length - LINE_SLOTS + 3) // 4,
+                    torch.zeros_like(length))
+    v = torch.where(length > LINE_ENTS, 1 + (length - LINE_ENTS), torch.zeros_like(length))
+    return torch.where(hub, v, p)
 
-    def __init__(self, A: Interactions, lam: float, tile: int):
+
+class TileWeights:
+    """general_W restricted to one item tile, in the line format of csrc/spread_tiled.hip
+    (lg_spread_tile_rows_f64: one 128-byte line per item row at 128 * i, plus overflow runs;
+    P rows = the (user, item) pairs behind the row as 4-byte slots, V rows = the merged fp64
+    general_W values of hub items). The tile itself is lambda-independent; ``lam`` sets the
+    HybridScale that resource() applies. build() moves to the next tile; the buffers are
+    reused and grown on demand. ``vthr``: rows with more pairs are V rows (default: the tile
+    width; LGCNHS_V_THRESHOLD overrides)."""
+
+    def __init__(self, A: Interactions, lam: float, tile: int, vthr: int | None = None):
         if not 1 <= tile <= 8192:
             raise ValueError(f"tile {tile} not in [1, 8192]")
-        self.A, self.tile = A, int(tile)
+        self.A, self.tile, self.lam = A, int(tile), float(lam)
         dev = A.k_item.device
         self.dev = dev
-        self.alpha, self.beta = hybrid_factors(A.k_item, lam)
+        if vthr is None:
+            vthr = int(os.environ.get("LGCNHS_V_THRESHOLD", "0")) or self.tile
+        self.vthr = max(LINE_SLOTS, int(vthr))
         I = A.n_items
         self.cur = A.by_user.rowptr[:-1].contiguous().clone()
         self.end = torch.empty_like(self.cur)
@@ -396,67 +434,71 @@ class TileWeights:
                 "lg_inv_degree_f64")
         self.user_cls, self.inv_cls = degree_classes(A.by_user.degrees())
         self.bound = torch.empty(I, dtype=torch.int64, device=dev)
-        self.ptr = torch.zeros(I + 1, dtype=torch.int64, device=dev)
-        self.meta = torch.empty((I, 2), dtype=torch.int64, device=dev)  # {ptr|len<<40|V<<63, alpha}
-        self.ws = torch.empty(max(1, N.lib().lg_spread_tile_weight_ws_bytes(I)),
+        self.ovf_ptr = torch.zeros(I, dtype=torch.int64, device=dev)
+        # I + 1 lines: line I (the walk's padding row) stays all zero
+        self.lines = torch.empty((I + 1) * 32, dtype=torch.int32, device=dev)
+        self.lines[I * 32:].zero_()
+        self.row_len = torch.empty(max(1, I), dtype=torch.int32, device=dev)
+        self.ws = torch.empty(max(1, N.lib().lg_spread_tile_rows_ws_bytes(I)),
                               dtype=torch.uint8, device=dev)
-        self.ent = torch.empty(0, dtype=torch.int32, device=dev)  # 4-byte slots
+        self.ovf = torch.zeros(64 * 4, dtype=torch.int32, device=dev)
+        self.n_units = 0
         self.j0 = None
         self.width = 0
         self._seek_at = None
-        # Rows start on 128-B lines (32 slots): a P row of n pairs then spans ceil(4n / 128)
-        # lines instead of one more on average at a random start.
-        self.align = int(os.environ.get("LGCNHS_W_ALIGN", "32"))
-        if self.align < 1 or self.align & (self.align - 1):
-            raise ValueError(f"LGCNHS_W_ALIGN={self.align}: a power of two")
+        self._scale = None
+        self.row_uses = None  # set by spread_topk_tiled(stats=...)
 
     @property
-    def len(self) -> torch.Tensor:
-        """Slots of each row in the current tile."""
-        return ((self.meta[:, 0] >> 40) & ((1 << 23) - 1)).to(torch.int64)
+    def scale(self) -> HybridScale:
+        if self._scale is None:
+            self._scale = HybridScale(self.A, self.lam)
+        return self._scale
 
     @property
     def is_hub(self) -> torch.Tensor:
-        """True for V (merged-value) rows."""
-        return self.meta[:, 0] < 0
+        """True for V (merged-value) rows of the current tile."""
+        return self.bound > self.vthr
 
     def dense(self) -> torch.Tensor:
-        """The current tile of W as a dense [I, width] fp64 matrix (host, test helper): P
-        runs summed in slot order and divided by alpha_i * beta_j exactly as the walk does,
-        V values as stored."""
-        meta = self.meta.cpu()
-        ptr = (meta[:, 0] & ((1 << 40) - 1)).numpy()
-        ln = ((meta[:, 0] >> 40) & ((1 << 23) - 1)).numpy()
-        hub = (meta[:, 0] < 0).numpy()
-        alpha = meta[:, 1].contiguous().view(torch.float64).numpy()
-        beta = self.beta.cpu().numpy()[self.j0:self.j0 + self.width]
+        """general_W of the current tile as a dense [I, width] fp64 matrix (host, test
+        helper), decoded from the lines with the format invariants checked: P slots summed in
+        slot order (users ascending: lg_spread_general_f64's order), V values as stored."""
+        I = self.A.n_items
+        lines = self.lines[:I * 32].cpu().numpy().view(np.uint32).reshape(I, 32)
+        ovf = self.ovf.cpu().numpy().view(np.uint32)
         inv = self.inv_cls.cpu().numpy()
-        ent = self.ent.cpu().numpy().view(np.uint32)
-        out = np.zeros((self.A.n_items, self.width))
-        for i in np.nonzero(ln)[0]:
-            sl = ent[ptr[i]:ptr[i] + ln[i]]
-            if hub[i]:
-                t = sl.reshape(-1, 3)
-                assert np.all((t[:, 0] >> 16) & 0x3FFF == 0x3FFF)
-                col = (t[:, 0] & 0xFFFF).astype(np.int64)
-                gw = (t[:, 1].astype(np.uint64) | (t[:, 2].astype(np.uint64) << 32)).view(np.float64)
-                assert np.all(np.diff(col) > 0)
-                den = alpha[i] * beta[col]
-                out[i, col] = gw / np.where(den != 0.0, den, 1.0)
+        rl = self.row_len.cpu().numpy()
+        hub = self.is_hub.cpu().numpy()
+        out = np.zeros((I, self.width))
+        for i in range(I):
+            h = int(lines[i, 0])
+            isv, has, slow, ou = h >> 31, (h >> 30) & 1, (h >> 29) & 1, h & 0x1FFFFFFF
+            assert bool(isv) == bool(hub[i]) and (slow or not isv)
+            run = np.zeros((0, 4), np.uint32)
+            if has:
+                n = int(ovf[4 * ou])
+                assert np.all(ovf[4 * ou + 1:4 * ou + 4] == 0)
+                run = ovf[4 * (ou + 1):4 * (ou + 1 + n)].reshape(n, 4)
+            if isv:
+                assert np.all(lines[i, 1:4] == 0)
+                units = np.concatenate([lines[i, 4:].reshape(7, 4), run])
+                units = units[units[:, 0] != 0]
+                assert units.shape[0] == rl[i] and np.all(units[:, 0] >> 31 == 1)
+                col = (units[:, 0] & 0xFFFF).astype(np.int64)
+                assert np.all(np.diff(col) > 0) and np.all(col < self.width)
+                out[i, col] = (units[:, 1].astype(np.uint64) |
+                               (units[:, 2].astype(np.uint64) << 32)).view(np.float64)
                 continue
-            col = (sl & 0xFFFF).astype(np.int64)
-            cls = (sl >> 16) & 0x3FFF
-            cont = (sl >> 31) & 1
-            nxt = (sl >> 30) & 1
-            assert np.all(np.diff(col) >= 0) and np.all(col < self.width)
-            assert np.array_equal(cont[1:], nxt[:-1]) and cont[0] == 0 and nxt[-1] == 0
-            assert np.all((np.diff(col) == 0) == (cont[1:] == 1))
-            s, c0 = 0.0, -1
-            for t in range(sl.size):
-                s = inv[cls[t]] if not cont[t] else s + inv[cls[t]]
-                if not nxt[t]:
-                    den = alpha[i] * beta[col[t]]
-                    out[i, col[t]] = s / (den if den != 0.0 else 1.0)
+            words = np.concatenate([lines[i, 1:], run.reshape(-1)])
+            n = int(rl[i])
+            assert np.all(words[:n] != 0) and np.all(words[n:] == 0)
+            col = (words[:n] & 0xFFFF).astype(np.int64)
+            cls = (words[:n] >> 16).astype(np.int64)
+            assert np.all(col < self.width) and np.all(cls > 0)
+            assert bool(slow) == bool(np.any(cls >= INV_TAB))
+            for c, q in zip(col, cls):
+                out[i, c] += inv[q]
         return out
 
     def seek(self, j0: int) -> None:
@@ -495,36 +537,40 @@ class TileWeights:
         N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
                                        N.ptr(self.count), N.ptr(self.bound), strm),
                 "lg_spread_tile_bound")
-        # row capacities in slots: P rows hold their pairs, V (hub) rows one triple per
-        # distinct column
-        cap = torch.where(self.bound <= SORT_MAX, self.bound,
-                          3 * torch.clamp(self.bound, max=self.tile))
-        if self.align > 1:
-            cap = torch.bitwise_and(cap + (self.align - 1), -self.align)
-        torch.cumsum(cap, 0, out=self.ptr[1:])
-        total = int(self.ptr[-1])  # host sync: sizes the row storage
-        if total >= 1 << 40:
-            raise ValueError("tile too large for the 40-bit row pointers")
-        if total > self.ent.numel():
-            n = max(total, int(self.ent.numel() * 1.25))
-            self.ent = torch.empty(n, dtype=torch.int32, device=self.dev)
-        N.check(L.lg_spread_tile_weight_f64(
+        hub = self.bound > self.vthr
+        units = _run_units(torch.where(hub, torch.clamp(self.bound, max=width), self.bound), hub)
+        cum = torch.cumsum(units, 0)
+        torch.sub(cum, units, out=self.ovf_ptr)
+        total = int(cum[-1]) if I else 0  # host sync: sizes the overflow runs
+        if total + 64 >= 1 << 29:
+            raise ValueError("tile too large for the 29-bit overflow pointers (use a smaller tile)")
+        if (total + 64) * 4 > self.ovf.numel():
+            n = max((total + 64) * 4, int(self.ovf.numel() * 1.25))
+            self.ovf = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        self.n_units = total
+        N.check(L.lg_spread_tile_rows_f64(
             N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
             N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count),
-            N.ptr(self.alpha), N.ptr(self.beta), j0, self.tile, N.ptr(self.bound),
-            N.ptr(self.ptr), N.ptr(self.ent), N.ptr(self.meta), N.ptr(self.ws),
-            self.ws.numel(), strm), "lg_spread_tile_weight_f64")
+            j0, self.tile, N.ptr(self.bound), self.vthr, N.ptr(self.ovf_ptr), N.ptr(self.lines),
+            N.ptr(self.ovf), N.ptr(self.row_len), N.ptr(self.ws), self.ws.numel(), strm),
+            "lg_spread_tile_rows_f64")
         self.j0, self.width = j0, width
-        if getattr(self, "row_uses", None) is not None:
-            self.slots_read += (self.row_uses * self.len).sum()
+        if self.row_uses is not None:
+            ln = self.row_len[:I].to(torch.int64)
+            self.paths_read += (self.row_uses * ln).sum()
+            used = _run_units(ln, hub)
+            self.bytes_read += 128 * self.row_uses.sum() + 16 * (self.row_uses * used).sum()
 
-    def resource(self, u0: int, u1: int, out: torch.Tensor) -> torch.Tensor:
+    def resource(self, u0: int, u1: int, out: torch.Tensor,
+                 scale: HybridScale | None = None) -> torch.Tensor:
         """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
         A = self.A
+        sc = scale if scale is not None else self.scale
         N.check(N.lib().lg_spread_tile_resource_f64(
-            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), u1 - u0, N.ptr(self.meta),
-            N.ptr(self.ent), N.ptr(self.beta), N.ptr(self.inv_cls), self.j0, self.tile,
-            self.width, N.ptr(out), out.stride(0), N.stream_handle(self.dev)),
+            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), N.ptr(sc.ra_edge), u1 - u0,
+            N.ptr(self.lines), N.ptr(self.ovf), A.n_items, N.ptr(sc.rb), N.ptr(self.inv_cls),
+            self.j0,
+            self.tile, self.width, N.ptr(out), out.stride(0), N.stream_handle(self.dev)),
             "lg_spread_tile_resource_f64")
         return out
 
@@ -552,10 +598,11 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       items: slice | None = None, fused: bool | None = None,
                       stats: dict | None = None):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
-    never holds general_W, W (I x I) or F (U x I). Bitwise the result of
-    spread_topk(A, hybrid_weight(spread_general(A), A.k_item, lam), ...).
+    never holds general_W, W (I x I) or F (U x I). The values of spread_topk(A,
+    hybrid_weight(spread_general(A), A.k_item, lam), ...) within a few ulp (the walk's
+    summation order), the lists equal except near-ties.
 
-    Each tile of W (user-independent) is built once and walked by every user
+    Each tile of general_W (user-independent) is built once and walked by every user
     (lg_spread_tile_resource_topk_f64): the user's F columns are summed in LDS and merged
     into its running top-k list in the same pass. With a G factor (SpreadLightGCN) the
     per-(user, 64-column chunk) score bounds of lg_score_chunk_bound (bf16 MFMA) screen the
@@ -564,10 +611,11 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     candidates to an item range (the lists of disjoint item ranges merge, with
     merge_topk_lists, into the full lists: the multi-GPU item shard). fused=False keeps the
     two-kernel form (F columns of a span of tiles written to a [users, span] scratch of
-    ``scratch_bytes``, then lg_tile_topk_f64). ``stats`` (optional dict) receives
-    "w_slots_read": the 4-byte W slots the walk gathers, sum over tiles and users u of
-    sum_{i in items(u)} |row i of W in the tile| (= the (i, v, j) paths of F = A W, plus
-    the hub rows' merged triples)."""
+    ``scratch_bytes``, then lg_tile_topk_f64; the same F values, so the same lists).
+    ``stats`` (optional dict) receives "w_paths": the paths the walk adds (sum over tiles and
+    users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the tile) and
+    "w_bytes": the row bytes it gathers (one 128-byte line per (user, item) and tile, plus
+    16 bytes per overflow unit)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -577,7 +625,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     idxs = torch.full((n, k), -1, dtype=torch.int64, device=dev)
     if n == 0 or i1 <= i0:
         return vals, idxs
-    tile = min(int(tile), i1 - i0)
+    tile = min(int(tile), i1 - i0, 4096 if eu is not None else 8192)  # G: <= 64 chunk bounds
     tw = TileWeights(A, lam, tile)
     if i0:
         tw.seek(i0)
@@ -586,12 +634,18 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     if fused is None:
         fused = True
     if stats is not None:
-        # users of each item among [u0, u1): the times its W row is gathered per tile
+        # users of each item among [u0, u1): the times its row is gathered per tile
         cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
         tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
-        tw.slots_read = torch.zeros((), dtype=torch.int64, device=dev)
+        tw.paths_read = torch.zeros((), dtype=torch.int64, device=dev)
+        tw.bytes_read = torch.zeros((), dtype=torch.int64, device=dev)
     if fused:
-        _fused_walk(A, tw, u0, u1, i0, i1, k, ex if drop else None, eu_r, ei, vals, idxs)
+        walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile)
+        for j0 in range(i0, i1, tile):
+            tw.build(j0, stop=i1)
+            walk.step(tw.lines, tw.ovf, tw.inv_cls, tw.scale, j0, tile, tw.width, j0 == i0)
+        vals.copy_(walk.vals)
+        idxs.copy_(walk.idxs)
     else:
         span = max(tile, scratch_bytes // (n * 8) // tile * tile)
         span = min(span, -(-(i1 - i0) // tile) * tile)
@@ -603,7 +657,8 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                 tw.resource(u0, u1, F[:, j0 - s0:])
             tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
     if stats is not None:
-        stats["w_slots_read"] = stats.get("w_slots_read", 0) + int(tw.slots_read)
+        stats["w_paths"] = stats.get("w_paths", 0) + int(tw.paths_read)
+        stats["w_bytes"] = stats.get("w_bytes", 0) + int(tw.bytes_read)
     return vals, idxs
 
 
@@ -643,10 +698,11 @@ def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
 
 
 class TileWalk:
-    """The fused top-K walk of users [u0, u1) over W tiles (lg_spread_tile_resource_topk_f64
-    per tile, with lg_score_chunk_bound screening when there is a G factor). Holds the
-    running lists (vals fp64 / idxs int64 [n, k]), the per-user exclusion cursors and the
-    bf16 score operands, so several walks (a lambda sweep) can share them."""
+    """The fused top-K walk of users [u0, u1) over general_W tiles
+    (lg_spread_tile_resource_topk_f64 per tile, with lg_score_chunk_bound screening when
+    there is a G factor). Holds the running lists (vals fp64 / idxs int64 [n, k]), the
+    per-user exclusion cursors and the bf16 score operands, so several walks (a lambda sweep)
+    can share them."""
 
     def __init__(self, A: Interactions, u0: int, u1: int, i0: int, k: int,
                  ex: RowSets | None, eu=None, ei=None, tile: int = 2048):
@@ -686,33 +742,21 @@ class TileWalk:
         return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
                             self.gbuf)
 
-    def step(self, meta, ent, beta, inv_cls, j0: int, tile: int, width: int, first: bool,
-             gb: torch.Tensor | None = None) -> None:
-        """Merge tile [j0, j0 + width) (its W rows: meta / ent) into the lists."""
+    def step(self, lines, ovf, inv_cls, scale: HybridScale, j0: int, tile: int, width: int,
+             first: bool, gb: torch.Tensor | None = None) -> None:
+        """Merge tile [j0, j0 + width) (its rows: lines / ovf) into the lists."""
         A, ex = self.A, self.ex
         if self.d and gb is None:
             gb = self.bounds(j0, width)
         nch = gb.shape[1] if gb is not None else 0
         N.check(N.lib().lg_spread_tile_resource_topk_f64(
-            N.ptr(A.by_user.rowptr[self.u0:]), N.ptr(A.by_user.col), self.n, N.ptr(meta),
-            N.ptr(ent), N.ptr(beta), N.ptr(inv_cls), int(j0), int(tile), int(width),
-            N.ptr(self.eu), N.ptr(self.ei), self.d, N.ptr(gb), nch,
+            N.ptr(A.by_user.rowptr[self.u0:]), N.ptr(A.by_user.col), N.ptr(scale.ra_edge),
+            self.n, N.ptr(lines), N.ptr(ovf), A.n_items, N.ptr(scale.rb), N.ptr(inv_cls), int(j0),
+            int(tile), int(width), N.ptr(self.eu), N.ptr(self.ei), self.d, N.ptr(gb), nch,
             N.ptr(ex.rowptr if ex is not None else None),
             N.ptr(ex.col if ex is not None else None), N.ptr(self.ex_cur), self.k,
             int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), N.stream_handle(self.dev)),
             "lg_spread_tile_resource_topk_f64")
-
-
-def _fused_walk(A: Interactions, tw: TileWeights, u0: int, u1: int, i0: int, i1: int, k: int,
-                ex: RowSets | None, eu, ei, vals: torch.Tensor, idxs: torch.Tensor) -> None:
-    """Tiles [i0, i1) of the factored spreading with the top-K merge fused into the walk
-    (one lg_score_chunk_bound + lg_spread_tile_resource_topk_f64 per tile)."""
-    walk = TileWalk(A, u0, u1, i0, k, ex, eu, ei, tw.tile)
-    for j0 in range(i0, i1, tw.tile):
-        tw.build(j0, stop=i1)
-        walk.step(tw.meta, tw.ent, tw.beta, tw.inv_cls, j0, tw.tile, tw.width, j0 == i0)
-    vals.copy_(walk.vals)
-    idxs.copy_(walk.idxs)
 
 
 def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
@@ -724,11 +768,10 @@ def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
     lambda), reusing what does not depend on lambda:
       dense  general_W (lg_spread_general_f64) once; per lambda W (lg_hybrid_weight_f64) and
              the fused F / top-k.
-      tiled  the W tiles hold only lambda-independent data (the (user, item) pair slots and
-             hub rows' general_W sums; alpha_i = k_i^(1-lam) sits in RowMeta and beta_j in
-             the walk's LDS table), so the tiles and the score bounds are built once and
-             cached on the device while they fit ``cache_bytes`` (default: half the free
-             memory); per lambda only alpha / beta change. If the cache does not fit, each
+      tiled  the general_W tiles (lambda-independent: ra / rb are applied by the walk) and
+             the score bounds are built once and cached on the device while they fit
+             ``cache_bytes`` (default: half the free memory); per lambda only the HybridScale
+             (ra per interaction, rb per item) changes. If the cache does not fit, each
              lambda rebuilds the tiles.
     Every result is bitwise the one spread_recommend(A, lam, ...) returns."""
     lams = [float(x) for x in lams]
@@ -746,30 +789,29 @@ def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
     if cache_bytes is None:
         cache_bytes = torch.cuda.mem_get_info(dev)[0] // 2
     U, I = A.n_users, A.n_items
-    tile = min(int(tile), I) if I else 1
+    tile = min(int(tile), I, 4096 if eu is not None else 8192) if I else 1
     ex = excl if drop else None
     walk = TileWalk(A, 0, U, 0, k, ex, eu, ei, tile)
     cache, used, cached = [], 0, True
+    inv_cls = None
     for n, lam in enumerate(lams):
-        alpha, beta = hybrid_factors(A.k_item, lam)
+        scale = HybridScale(A, lam)
         walk.reset()
         if n > 0 and cached:
-            for (j0, width, meta, ent, gb) in cache:
-                meta[:, 1].copy_(alpha.view(torch.int64))
-                walk.step(meta, ent, beta, inv_cls, j0, tile, width, j0 == 0, gb)
+            for (j0, width, lines, ovf, gb) in cache:
+                walk.step(lines, ovf, inv_cls, scale, j0, tile, width, j0 == 0, gb)
         else:
             tw = TileWeights(A, lam, tile)
             inv_cls = tw.inv_cls
             for j0 in range(0, I, tile):
                 tw.build(j0)
                 gb = walk.bounds(j0, tw.width)
-                walk.step(tw.meta, tw.ent, tw.beta, tw.inv_cls, j0, tile, tw.width, j0 == 0,
-                          gb)
+                walk.step(tw.lines, tw.ovf, inv_cls, scale, j0, tile, tw.width, j0 == 0, gb)
                 if n == 0 and cached and len(lams) > 1:
-                    total = int(tw.ptr[-1])
-                    need = total * 4 + tw.meta.numel() * 8 + (gb.numel() * 4 if gb is not None else 0)
+                    nov = (tw.n_units + 64) * 4
+                    need = tw.lines.numel() * 4 + nov * 4 + (gb.numel() * 4 if gb is not None else 0)
                     if used + need <= cache_bytes:
-                        cache.append((j0, tw.width, tw.meta.clone(), tw.ent[:total].clone(),
+                        cache.append((j0, tw.width, tw.lines.clone(), tw.ovf[:nov].clone(),
                                       None if gb is None else gb.clone()))
                         used += need
                     else:
@@ -809,7 +851,8 @@ def spread_recommend(A: Interactions, lam: float, k: int, excl: RowSets | None,
                      tiled: bool | None = None):
     """Per-user top-k of (G *) A @ HybridS(A, general_W(^T), lam), dense (I x I matrices on
     the device) or factored over item tiles (tiled=None: dense when it fits). The two
-    paths give the same bits. general_W is exactly symmetric (entry (i, j) and (j, i) are
+    paths give the same values within a few ulp (the factored walk sums each column's paths
+    in its own order) and the same lists except near-ties. general_W is exactly symmetric (entry (i, j) and (j, i) are
     the same sum, over the common users ascending, of the same fl(1/k_v)), so the
     reference's general_W.T overrides (model/SpreadMethod/recommend.py:89-91, :99-101)
     are served by either path unchanged."""

@@ -48,7 +48,7 @@ def spread_lightgcn_topk(model, user_num: int, item_num: int, train_data_df: pd.
         torch.from_numpy(both["item_id"].to_numpy(np.int64)), user_num, item_num, dev)
     eu = model.users_emb.weight.detach().to(dev, torch.float32).contiguous()
     ei = model.items_emb.weight.detach().to(dev, torch.float32).contiguous()
-    # dense I x I general_W / W when they fit, else the factored tile path (same bits)
+    # dense I x I general_W / W when they fit, else the factored tile path (same values within a few ulp)
     return ops.spread_recommend(inter, lambda_val, k, inter.by_user, drop=True, eu=eu, ei=ei,
                                 tiled=tiled)
 

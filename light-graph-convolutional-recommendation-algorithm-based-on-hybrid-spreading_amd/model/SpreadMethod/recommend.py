@@ -59,7 +59,7 @@ def spread_method_topk(user_num: int, item_num: int, train_data_df: pd.DataFrame
     elif method == "HeatS" and dataset == "douban":  # reference :97-101
         lambda_val, transpose = 0.99, True
     excl = inter.by_user  # train|val positives == the nonzeros of A
-    # dense I x I general_W / W when they fit, else the factored tile path (same bits)
+    # dense I x I general_W / W when they fit, else the factored tile path (same values within a few ulp)
     return ops.spread_recommend(inter, lambda_val, k, excl, drop=not unfiltered,
                                 transpose=transpose, tiled=tiled)
 

@@ -77,7 +77,7 @@ def main():
             e2.synchronize()
             t_build += e0.elapsed_time(e1) / 1e3
             t_res += e1.elapsed_time(e2) / 1e3
-            entries += int(tw.len.sum())
+            entries += int(tw.row_len[:I].sum())
             tiles += 1
         e0, e1 = ev(), ev()
         e0.record()

@@ -40,4 +40,4 @@ for rep in range(a.reps):
     torch.cuda.synchronize()
     dt = time.time() - t
     print(f"rep {rep}: {a.tiles} tiles x {U} users: {dt:.3f} s"
-          + (f"  slots {st['w_slots_read']:.3e}" if st else ""), flush=True)
+          + (f"  paths {st['w_paths']:.3e} bytes {st['w_bytes']:.3e}" if st else ""), flush=True)

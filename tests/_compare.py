@@ -67,3 +67,39 @@ def compare_topk_exact(got, ref, exact, tol, label=""):
     print(f"[{label}] tie-affected users: {ties} of {ref.shape[0]}")
     assert not bad, f"{label}: {len(bad)} users differ beyond rounding ties, first: {bad[:3]}"
     return ties, ref.shape[0]
+
+
+def compare_lists_close(got_v, got_i, ref_v, ref_i, rtol=1e-12, label=""):
+    """Two sorted top-k lists of the same scores computed in different summation orders
+    (e.g. the factored K3s walk against the dense spreading path): per row the same number
+    of entries, values position-wise within rtol, and the same item sets except near-ties,
+    where every differing item's value lies within rtol of the reference row's k-th value.
+    Returns the number of tie-affected rows (printed)."""
+    got_v, got_i = np.asarray(got_v), np.asarray(got_i)
+    ref_v, ref_i = np.asarray(ref_v), np.asarray(ref_i)
+    assert got_v.shape == ref_v.shape == got_i.shape == ref_i.shape
+    ties, bad = 0, []
+    for u in range(ref_v.shape[0]):
+        mg, mr = got_i[u] >= 0, ref_i[u] >= 0
+        if mg.sum() != mr.sum():
+            bad.append((u, "lengths", int(mg.sum()), int(mr.sum())))
+            continue
+        vg, vr = got_v[u][mg], ref_v[u][mr]
+        scale = np.maximum(np.abs(vr), np.finfo(np.float64).tiny)
+        if not np.all(np.abs(vg - vr) <= rtol * scale):
+            bad.append((u, "values", float(np.max(np.abs(vg - vr) / scale))))
+            continue
+        g, r = set(got_i[u][mg].tolist()), set(ref_i[u][mr].tolist())
+        if g == r:
+            continue
+        vk = vr[-1]
+        val = dict(zip(got_i[u][mg].tolist(), vg.tolist()))
+        val.update(zip(ref_i[u][mr].tolist(), vr.tolist()))
+        if all(abs(val[x] - vk) <= rtol * max(abs(vk), np.finfo(np.float64).tiny) for x in g ^ r):
+            ties += 1
+            continue
+        bad.append((u, "items", sorted(g - r), sorted(r - g)))
+    if label:
+        print(f"[{label}] tie-affected rows: {ties} of {ref_v.shape[0]}")
+    assert not bad, f"{label}: {len(bad)} rows differ beyond rounding, first: {bad[:3]}"
+    return ties
