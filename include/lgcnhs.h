@@ -322,7 +322,9 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
  * io_val/io_idx [n_users][k] (first != 0: start empty); F is never written to memory. G
  * factor: eu = the rows' user embeddings, ei = all item embeddings, gb =
  * lg_score_chunk_bound's [n_users][n_chunks] bounds for this tile (n_chunks =
- * ceil(width / 64) <= 64): only columns with gb * F > the K-th value get the exact score chain.
+ * ceil(width / 64) <= 64) and optionally qb/qstride, its per-column 8-bit bounds: only
+ * columns whose bound (gb * q / 255 with qb) times F can beat the K-th value get the exact
+ * score chain.
  * Exclusions (dropped): ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row cursor
  * ex_cur[n_users] positioned at the walk's first item by lg_spread_tile_seek(ex_rowptr,
  * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
@@ -337,6 +339,7 @@ int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *
                                      const double *inv_cls, int32_t item_begin, int32_t tile,
                                      int32_t width, const float *eu, const float *ei,
                                      int32_t dim, const float *gb, int32_t n_chunks,
+                                     const uint8_t *qb, int32_t qstride,
                                      const int64_t *ex_rowptr, const int32_t *ex_col,
                                      int64_t *ex_cur, int32_t k, int32_t first,
                                      double *io_val, int64_t *io_idx, lg_stream_t stream);
@@ -349,10 +352,14 @@ int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
 /* gb[u][c] (fp32, [n_users][ceil(width / 64)]) >= the fp32 score chain e0_u . e0_j of every
  * column j of chunk c = [item_begin + 64c, item_begin + 64c + 64) of the tile: the bf16 MFMA
  * product's chunk maximum plus a rigorous rounding margin (csrc/gbound.hip). u/i from
- * lg_bound_prep_f32 of the users' rows and of all items. dim in {32, 64, 128}. */
+ * lg_bound_prep_f32 of the users' rows and of all items. dim in {32, 64, 128}. qb (optional,
+ * [n_users][qstride] bytes, qstride >= width rounded up to 256): per column j,
+ * q = ceil(255 (G_bf16 + margin) / gb) in [0, 255], so gb * q / 255 >= the chain score too
+ * (csrc/gbound.hip). */
 int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
                          const void *i_bf16, const float *i_norm, int32_t dim,
-                         int32_t item_begin, int32_t width, float *gb, lg_stream_t stream);
+                         int32_t item_begin, int32_t width, float *gb, uint8_t *qb,
+                         int32_t qstride, lg_stream_t stream);
 
 /* out[r] = ||x[r]||_2 (fp64) for an fp32 [n_rows, dim] matrix. */
 int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,

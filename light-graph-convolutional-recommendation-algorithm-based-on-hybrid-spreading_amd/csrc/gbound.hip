@@ -10,6 +10,10 @@
 //                      <= 0.00785 ||u|| ||j||           (gamma_128 = 128 * 2^-24)
 // so gb = max_{j in c} G_bf16 + 0.008 ||u|| max_{j in c} ||j|| (norms rounded up to fp32),
 // nudged up by 2^-22 relative for the fp32 operations that formed it, is an upper bound.
+// Per column (optional qb): q_j = ceil(255 (G_bf16_j + the same margin) / gb (1 + 2^-20)),
+// clamped to [0, 255], so gb * q_j / 255 >= G_chain_j as well (q_j = 0 when the bound is
+// <= 0; gb <= 0 makes every column's bound <= 0). Stored row-major, one byte per column,
+// rows of qstride bytes.
 // Then fl(G_chain * F) <= fl(gb * F) for every F >= 0 (rounding is monotone), so a column
 // with gb * F <= tau can not beat tau. Cost per tile: 2 * U * T * D flop on bf16 MFMA
 // (v_mfma_f32_16x16x32_bf16: 16 items x 16 users x 32 dims per instruction; 64 users per
@@ -60,7 +64,8 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
                                                      const __bf16 *__restrict__ ib,
                                                      const float *__restrict__ inorm,
                                                      int32_t item_begin, int32_t width,
-                                                     int32_t nch, float *__restrict__ gb) {
+                                                     int32_t nch, float *__restrict__ gb,
+                                                     uint8_t *__restrict__ qb, int32_t qstride) {
   constexpr int S = D / 32;  // k-steps
   const int lane = lane_id();
   const int64_t ubase = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 64;
@@ -84,6 +89,7 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) inm = fmaxf(inm, __shfl_xor(inm, o));
     float gmax[4];
+    f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
     for (int g = 0; g < 4; ++g) gmax[g] = -__builtin_huge_valf();
 #pragma unroll
@@ -101,6 +107,7 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
 #pragma unroll
         for (int s = 0; s < S; ++s)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[s], bfr[g][s], acc, 0, 0, 0);
+        accs[t][g] = acc;
         // lane holds rows (items) 4*kg + r of this 16-item tile, column (user) ul
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -112,10 +119,28 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
       float m = gmax[g];
       m = fmaxf(m, __shfl_xor(m, 16));
       m = fmaxf(m, __shfl_xor(m, 32));
-      float b = m + kBoundMargin * un[g] * inm;
+      const float marg = kBoundMargin * un[g] * inm;
+      float b = m + marg;
       b += fabsf(b) * 0x1p-22f + 1e-30f;
       const int64_t uu = ubase + 16 * g + ul;
       if (kg == 0 && uu < n_users) gb[uu * nch + c] = b;
+      if (qb) {
+        // per column: 4 consecutive items of one user per lane and tile -> one dword
+        const float sc = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) : 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = (accs[t][g][r] + marg) * sc * (1.f + 0x1p-20f);
+            const float qf = fminf(fmaxf(ceilf(v), 0.f), 255.f);
+            w |= (uint32_t)qf << (8 * r);
+          }
+          const int col = cb + 16 * t + 4 * kg;
+          if (uu < n_users && col < qstride)
+            *reinterpret_cast<uint32_t *>(qb + uu * qstride + col) = w;
+        }
+      }
     }
   }
 }
@@ -136,11 +161,13 @@ extern "C" int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, vo
 
 extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
                                     const void *i_bf16, const float *i_norm, int32_t dim,
-                                    int32_t item_begin, int32_t width, float *gb,
-                                    lg_stream_t stream) {
+                                    int32_t item_begin, int32_t width, float *gb, uint8_t *qb,
+                                    int32_t qstride, lg_stream_t stream) {
   LG_REQUIRE(u_bf16 && u_norm && i_bf16 && i_norm && gb && n_users >= 0 && item_begin >= 0 &&
                  width >= 1,
              "lg_score_chunk_bound: bad arguments");
+  LG_REQUIRE(!qb || (qstride >= (width + 255) / 256 * 256 && qstride % 4 == 0),
+             "lg_score_chunk_bound: qstride %d < width %d rounded up to 256", qstride, width);
   LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_chunk_bound: dim %d not in "
              "{32,64,128}", dim);
   if (n_users == 0) return LG_OK;
@@ -149,9 +176,9 @@ extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int
   hipStream_t s = (hipStream_t)stream;
   const __bf16 *u = (const __bf16 *)u_bf16, *i = (const __bf16 *)i_bf16;
   switch (dim) {
-    case 32: k_chunk_bound<32><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
-    case 64: k_chunk_bound<64><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
-    default: k_chunk_bound<128><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb); break;
+    case 32: k_chunk_bound<32><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
+    case 64: k_chunk_bound<64><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
+    default: k_chunk_bound<128><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
   }
   return launch_status("lg_score_chunk_bound");
 }

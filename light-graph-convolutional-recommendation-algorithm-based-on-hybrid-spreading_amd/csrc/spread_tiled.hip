@@ -691,6 +691,8 @@ struct WalkArgs {
   const float *eu, *ei;       // rows' user embeddings / all item embeddings (or NULL)
   const float *gb;            // [n_users][nch] score bounds (with eu)
   int32_t nch;
+  const uint8_t *qb;          // [n_users][qstride] per-column 8-bit bounds (or NULL)
+  int32_t qstride;
   const int64_t *ex_rowptr;   // exclusions (dropped), with a per-row cursor
   const int32_t *ex_col;
   int64_t *ex_cur;
@@ -698,15 +700,16 @@ struct WalkArgs {
   double *io_val;
   int64_t *io_idx;
   int dbg;  // measurement knob (LGCNHS_WALK_DBG): 1 = no LDS atomics, 2 = no decode, 4 = no
-            // scan, 16 = plain LDS stores, 32 = atomics to conflict-free addresses
+            // scan, 16 = plain LDS stores, 32 = atomics to conflict-free addresses,
+            // 64 = no exact G score, 128 = no G candidates
 };
 
-// per wave: acc[tile], the overflow list (decode), the user's embedding and the scoring
-// queue (MODE_TOPK with D > 0; the running list itself lives in registers)
+// per wave: acc[tile], the overflow list (decode) and the user's embedding (MODE_TOPK with
+// D > 0; the running list itself lives in registers)
 template <int MODE, int D, int M>
 __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
   return ((size_t)tile * 8 + (size_t)kOvfList * 12 +
-          (MODE == MODE_TOPK && D > 0 ? (size_t)D * 4 + (size_t)128 * 12 : 0) + 15) &
+          (MODE == MODE_TOPK && D > 0 ? (size_t)D * 4 : 0) + 15) &
          ~(size_t)15;
 }
 __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
@@ -781,10 +784,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   double *acc = reinterpret_cast<double *>(mine);
   double *ovl_ra = acc + tile;  // overflow list (decode)
   uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
-  float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);
-  double *pf = reinterpret_cast<double *>(us + (D > 0 ? D : 0));  // candidate queue (D > 0)
-  int *pj = reinterpret_cast<int *>(pf + 128);
-  (void)us; (void)pf; (void)pj;
+  float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);  // the user's row (D > 0)
+  (void)us;
 
   for (int c = threadIdx.x; c < kInvTab; c += blockDim.x) s_inv[c] = a.g_inv[c];
   double rmax = 0.0;  // the tile's largest rb (top-K prefilter)
@@ -850,6 +851,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   int lid0 = -1, lid1 = -1;
   double lv0 = 0.0, lv1 = 0.0;
   float gbv = 0.f;
+  uint32_t qd0 = 0xFFFFFFFFu;  // the per-column bounds of columns 4 lane .. + 3 (D > 0)
   int64_t xpos = 0, xhi = 0;
   int32_t xw = 0x7fffffff;
   auto load_user = [&](int64_t u) __attribute__((always_inline)) {
@@ -870,7 +872,10 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           if (64 + lane >= k) lid1 = -1;
         }
       }
-      if constexpr (D > 0) gbv = a.gb[u * a.nch + (lane < a.nch ? lane : 0)];
+      if constexpr (D > 0) {
+        gbv = a.gb[u * a.nch + (lane < a.nch ? lane : 0)];
+        if (a.qb) qd0 = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + 4 * lane);
+      }
       if (a.ex_rowptr) {
         xpos = a.ex_cur[u];
         xhi = a.ex_rowptr[u + 1];
@@ -1032,13 +1037,13 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         if (lane >= k) { L0 = neg_inf<double>(); I0 = kPadId; }
         kth(tau, tau_id);
       };
-      bool us_ready = false;  // the user's embedding row is copied to LDS at the first flush
+      bool us_ready = false;  // the user's embedding row is copied to LDS at the first score
       // excluded items of this tile (the next run of the user's sorted exclusion row): -1
       const int32_t lim = a.item_begin + a.width;
       if (a.ex_rowptr) {
         for (;;) {
           const bool in = xw < lim;
-          if (in && xw >= a.item_begin) acc[xw - a.item_begin] = -1.0;
+          if (in && xw >= a.item_begin) acc[xw - a.item_begin] = neg_inf<double>();
           const int nin = __popcll(__ballot(in));
           xpos += nin;
           if (nin < 64) break;
@@ -1053,8 +1058,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       // fl(gb fl(acc rb_j)) > tau is covered by the 2^-50 margin); those get rb_j and (with G)
       // the exact score. The list order (value desc, id asc) is total, so the order in which
       // candidates are inserted does not matter.
-      int np = 0;  // scoring queue (D > 0)
-      auto flush = [&](int m) __attribute__((always_inline)) {
+      // the user's embedding row, copied to LDS before its first exact score (D > 0)
+      auto need_us = [&]() __attribute__((always_inline)) {
         if constexpr (D > 0) {
           if (!us_ready) {
             const float e0 = a.eu[u * D + (lane < D ? lane : 0)];
@@ -1064,104 +1069,113 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
               if (64 + lane < D) us[64 + lane] = e1;
             }
             us_ready = true;
-          }
-          wave_sync();
-          bool cand = lane < m;
-          double v = 0.0;
-          int item = 0;
-          if (cand) {
-            item = a.item_begin + pj[lane];
-            v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * pf[lane];
-          }
-          wave_sync();
-          if (np > 64) {  // keep the queue's tail
-            if (lane < np - 64) { pj[lane] = pj[64 + lane]; pf[lane] = pf[64 + lane]; }
-          }
-          np = np > 64 ? np - 64 : 0;
-          uint64_t bal = __ballot(cand && before(v, item, tau, tau_id));
-          while (bal) {
-            const int l = __ffsll((long long)bal) - 1;
-            bal &= bal - 1;
-            insert1(__shfl(v, l), __shfl(item, l));
+            wave_sync();
           }
         }
       };
-      // one column of a lane that passed the prefilter (pre: lanes with a candidate)
-      auto take = [&](bool pre, double sacc, int j, float gbc) __attribute__((always_inline)) {
-        if (!__ballot(pre)) return;
-        const double f = pre ? sacc * a.rbeta[a.item_begin + (pre ? j : 0)] : -1.0;
-        if constexpr (D > 0) {
-          const bool cand = pre && (double)gbc * f > tau;
-          const uint64_t bal = __ballot(cand);
-          if (bal) {
-            const int p = np + __popcll(bal & lanemask_lt());
-            if (cand) {
-              pj[p] = j;
-              pf[p] = f;
-            }
-            np += __popcll(bal);
-            if (np >= 64) flush(64);
-          }
-        } else {
-          uint64_t bal = __ballot(pre && before(f, a.item_begin + j, tau, tau_id));
-          while (bal) {
-            const int l = __ffsll((long long)bal) - 1;
-            bal &= bal - 1;
-            insert1(__shfl(f, l), a.item_begin + __shfl(j, l));
-          }
-        }
+      // The scan, 512 columns per iteration: lane l takes columns c0 + 4l .. + 3 and
+      // c0 + 256 + 4l .. + 3 (ds_read_b128 x 4). A column can enter only if
+      //   no G:  acc > thr = tau / (rb_max (1 + 2^-50))            (excluded: acc = -inf)
+      //   G:     acc * q * (rb_max (1 + 2^-50) max(gb, 0) / 255) > tau
+      // (gb * q / 255 >= the exact score, q = the column's 8-bit bound, 255 without qb; the
+      // 2^-50 margin covers every rounding of fl(G fl(acc rb_j)) > tau). The lanes' passing
+      // columns form a bit mask that one loop drains (one candidate per lane per round): rb_j,
+      // then (G) the column bound times f and the exact chain score, then the insertion. The
+      // list order (value desc, id asc) is total, so the insertion order does not matter.
+      double thr_s = tau / rscale;
+      double sc_v = 0.0, bq_v = 0.0;  // per 64-column chunk c in lane c (D > 0)
+      if constexpr (D > 0) {
+        const double gp = (double)fmaxf(gbv, 0.f);
+        sc_v = rscale * gp * (1.0 / 255.0);
+        bq_v = gp * (1.0 / 255.0) * (1.0 + 0x1p-50);
+      }
+      auto q_at = [&](int c0) __attribute__((always_inline)) {  // q dword of column c0 + 4l
+        uint32_t q = 0xFFFFFFFFu;
+        if constexpr (D > 0)
+          if (a.qb && c0 < a.qstride)
+            q = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + c0 + 4 * lane);
+        return q;
       };
-      // thresholds: no G, one per user (thr_s); with G, one per 64-column chunk c in lane c
-      // (thr_v); refreshed when tau moves
-      double thr_s = 0.0, thr_v = 0.0;
-      double tau_seen = 0.0;
-      auto refresh = [&]() __attribute__((always_inline)) {
-        if constexpr (D > 0) {
-          const double bnd = rscale * (double)fmaxf(gbv, 0.f);
-          const double t = tau / bnd;
-          thr_v = t > -0.5 ? t : -0.5;
-        } else {
-          const double t = tau / rscale;
-          thr_s = t > -0.5 ? t : -0.5;
-        }
-        tau_seen = tau;
-      };
-      refresh();
+      uint32_t qn0 = qd0, qn1 = q_at(256);
       const double2 zero2{0.0, 0.0};
       for (int c0 = 0; c0 < a.width; c0 += 512) {
-        double2 s4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = c0 + 128 * t + 2 * lane;
-          s4[t] = j < tile ? *reinterpret_cast<const double2 *>(acc + j) : double2{-1.0, -1.0};
+        const uint32_t qa = qn0, qb2 = qn1;
+        if (c0 + 512 < a.width) {  // the next iteration's bounds, in flight during this one
+          qn0 = q_at(c0 + 512);
+          qn1 = q_at(c0 + 768);
         }
+        double sv[8];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = c0 + 128 * t + 2 * lane;
-          if (j < tile) *reinterpret_cast<double2 *>(acc + j) = zero2;
-        }
+        for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = c0 + 128 * t + 2 * lane;
-          float gbc = 0.f;
-          double thr = thr_s;
-          if constexpr (D > 0) {
-            gbc = __shfl(gbv, (j >> 6) & 63);
-            thr = __shfl(thr_v, (j >> 6) & 63);
+          for (int pp = 0; pp < 2; ++pp) {
+            const int j = c0 + 256 * hh + 4 * lane + 2 * pp;
+            double2 x = double2{neg_inf<double>(), neg_inf<double>()};
+            if (j < tile) {
+              x = *reinterpret_cast<const double2 *>(acc + j);
+              *reinterpret_cast<double2 *>(acc + j) = zero2;
+            }
+            sv[4 * hh + 2 * pp] = j < a.width ? x.x : neg_inf<double>();
+            sv[4 * hh + 2 * pp + 1] = j + 1 < a.width ? x.y : neg_inf<double>();
           }
-          const double sx = j < a.width ? s4[t].x : -1.0;
-          const double sy = j + 1 < a.width ? s4[t].y : -1.0;
-          if (__ballot(sx > thr || sy > thr)) {
-            take(sx > thr, sx, j, gbc);
-            if (tau != tau_seen) refresh();
-            if constexpr (D > 0) thr = __shfl(thr_v, (j >> 6) & 63);
-            else thr = thr_s;
-            take(sy > thr, sy, j + 1, gbc);
-            if (tau != tau_seen) refresh();
+        double sc0 = 0.0, sc1 = 0.0;
+        if constexpr (D > 0) {
+          sc0 = __shfl(sc_v, ((c0 + 4 * lane) >> 6) & 63);
+          sc1 = __shfl(sc_v, ((c0 + 256 + 4 * lane) >> 6) & 63);
+        }
+        uint32_t mask = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          bool pre;
+          if constexpr (D > 0) {
+            const uint32_t qq = t < 4 ? qa : qb2;
+            const double qv = (double)((qq >> (8 * (t & 3))) & 0xFFu);
+            pre = sv[t] * qv * (t < 4 ? sc0 : sc1) > tau;
+          } else {
+            pre = sv[t] > thr_s;
+          }
+          mask |= pre ? 1u << t : 0u;
+        }
+        while (__ballot(mask != 0)) {
+          const bool has = mask != 0;
+          const int t = has ? __ffs(mask) - 1 : 0;
+          mask &= mask - 1;
+          double s = sv[0];
+#pragma unroll
+          for (int x = 1; x < 8; ++x) s = t == x ? sv[x] : s;
+          const int j = c0 + 256 * (t >> 2) + 4 * lane + (t & 3);
+          const double f = has ? s * a.rbeta[a.item_begin + (has ? j : 0)] : -1.0;
+          if constexpr (D > 0) {
+            const uint32_t qq = t < 4 ? qa : qb2;
+            const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
+                              __shfl(bq_v, (j >> 6) & 63);
+            const bool cand = has && bq * f > tau;
+            if (__ballot(cand)) {
+              need_us();
+              double v = 0.0;
+              const int item = a.item_begin + j;
+              if (cand) {
+                if (a.dbg & 64) v = f;  // (measurement: no exact score)
+                else v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * f;
+              }
+              uint64_t bal = __ballot(cand && before(v, item, tau, tau_id));
+              while (bal) {
+                const int l = __ffsll((long long)bal) - 1;
+                bal &= bal - 1;
+                insert1(__shfl(v, l), __shfl(item, l));
+              }
+            }
+          } else {
+            uint64_t bal = __ballot(has && before(f, a.item_begin + j, tau, tau_id));
+            while (bal) {
+              const int l = __ffsll((long long)bal) - 1;
+              bal &= bal - 1;
+              insert1(__shfl(f, l), a.item_begin + __shfl(j, l));
+            }
+            thr_s = tau / rscale;
           }
         }
       }
-      while (np > 0) flush(np < 64 ? np : 64);
       for (int j = a.width + lane; j < tile; j += 64) acc[j] = 0.0;  // (never touched)
       if (dirty) {
         if (lane < k) {
@@ -1571,7 +1585,8 @@ extern "C" int lg_spread_tile_resource_topk_f64(
     const int64_t *user_rowptr, const int32_t *user_items, const double *ra_edge,
     int64_t n_users, const void *lines, const void *ovf, int32_t null_row, const double *rbeta,
     const double *inv_cls, int32_t item_begin, int32_t tile, int32_t width, const float *eu,
-    const float *ei, int32_t dim, const float *gb, int32_t n_chunks, const int64_t *ex_rowptr,
+    const float *ei, int32_t dim, const float *gb, int32_t n_chunks, const uint8_t *qb,
+    int32_t qstride, const int64_t *ex_rowptr,
     const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
     int64_t *io_idx, lg_stream_t stream) {
   LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls &&
@@ -1587,6 +1602,8 @@ extern "C" int lg_spread_tile_resource_topk_f64(
              "lg_spread_tile_resource_topk_f64: dim %d not in {32,64,128}", dim);
   LG_REQUIRE(!eu || n_chunks == (width + 63) / 64,
              "lg_spread_tile_resource_topk_f64: n_chunks %d != ceil(width / 64)", n_chunks);
+  LG_REQUIRE(!qb || (eu && qstride >= (width + 255) / 256 * 256),
+             "lg_spread_tile_resource_topk_f64: qb needs eu and qstride >= width rounded to 256");
   LG_REQUIRE(!eu || n_chunks <= 64,
              "lg_spread_tile_resource_topk_f64: a G factor needs width <= 4096 (one chunk "
              "bound per lane), got %d", width);
@@ -1610,6 +1627,8 @@ extern "C" int lg_spread_tile_resource_topk_f64(
   a.ei = ei;
   a.gb = gb;
   a.nch = n_chunks;
+  a.qb = qb;
+  a.qstride = qstride;
   a.ex_rowptr = ex_rowptr;
   a.ex_col = ex_col;
   a.ex_cur = ex_cur;

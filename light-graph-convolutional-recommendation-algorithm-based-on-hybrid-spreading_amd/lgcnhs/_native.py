@@ -93,10 +93,10 @@ SIGNATURES = {
     "lg_spread_tile_resource_topk_f64": (
         ctypes.c_int,
         [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp,
-         _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+         _i32, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "lg_bound_prep_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "lg_score_chunk_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp,
-                                            _vp]),
+                                            _vp, _i32, _vp]),
     "lg_row_norms_f64": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "lg_rec_hits": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     "lg_rec_pair_overlap": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),

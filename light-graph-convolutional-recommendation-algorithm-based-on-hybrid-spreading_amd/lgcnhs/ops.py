@@ -683,18 +683,22 @@ def bound_operands(x: torch.Tensor):
 
 
 def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
-                 out: torch.Tensor | None = None) -> torch.Tensor:
+                 out: torch.Tensor | None = None, qout: torch.Tensor | None = None):
     """[users, ceil(width/64)] fp32 upper bounds of the fp32 score chain over each 64-column
-    chunk of items [j0, j0 + width) (lg_score_chunk_bound)."""
+    chunk of items [j0, j0 + width) (lg_score_chunk_bound); with qout ([users, qstride]
+    uint8, qstride >= width rounded up to 256) also the per-column 8-bit bounds. Returns gb,
+    or (gb, q) with qout."""
     n = ub.shape[0]
     nch = -(-width // 64)
     if out is None or out.numel() < n * nch:
         out = torch.empty(n * nch, dtype=torch.float32, device=ub.device)
     gb = out[:n * nch].view(n, nch)
+    qs = 0 if qout is None else qout.shape[1]
     N.check(N.lib().lg_score_chunk_bound(N.ptr(ub), N.ptr(un), n, N.ptr(ib), N.ptr(inorm),
                                          int(dim), int(j0), int(width), N.ptr(gb),
-                                         N.stream_handle(ub.device)), "lg_score_chunk_bound")
-    return gb
+                                         N.ptr(qout), int(qs), N.stream_handle(ub.device)),
+            "lg_score_chunk_bound")
+    return gb if qout is None else (gb, qout)
 
 
 class TileWalk:
@@ -721,6 +725,11 @@ class TileWalk:
             self.ib, self.inorm = bound_operands(self.ei)
             self.gbuf = torch.empty(self.n * -(-int(tile) // 64), dtype=torch.float32,
                                     device=self.dev)
+            # per-column 8-bit bounds (LGCNHS_COL_BOUNDS=0: chunk bounds only)
+            self.qbuf = None
+            if os.environ.get("LGCNHS_COL_BOUNDS", "1") != "0":
+                self.qbuf = torch.empty((self.n, -(-int(tile) // 256) * 256),
+                                        dtype=torch.uint8, device=self.dev)
         self.ex_cur = None
         if ex is not None:
             self.ex_cur = torch.empty(self.n, dtype=torch.int64, device=self.dev)
@@ -736,23 +745,30 @@ class TileWalk:
                                                 N.stream_handle(self.dev)),
                     "lg_spread_tile_seek")
 
-    def bounds(self, j0: int, width: int) -> torch.Tensor | None:
+    def bounds(self, j0: int, width: int):
+        """(gb, q) score bounds of tile [j0, j0 + width) (q None: chunk bounds only)."""
         if not self.d:
             return None
+        if self.qbuf is None:
+            return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
+                                self.gbuf), None
         return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
-                            self.gbuf)
+                            self.gbuf, self.qbuf)
 
     def step(self, lines, ovf, inv_cls, scale: HybridScale, j0: int, tile: int, width: int,
-             first: bool, gb: torch.Tensor | None = None) -> None:
-        """Merge tile [j0, j0 + width) (its rows: lines / ovf) into the lists."""
+             first: bool, bnd=None) -> None:
+        """Merge tile [j0, j0 + width) (its rows: lines / ovf) into the lists; bnd = the
+        tile's bounds() (computed here when None)."""
         A, ex = self.A, self.ex
-        if self.d and gb is None:
-            gb = self.bounds(j0, width)
+        if self.d and bnd is None:
+            bnd = self.bounds(j0, width)
+        gb, q = bnd if bnd is not None else (None, None)
         nch = gb.shape[1] if gb is not None else 0
         N.check(N.lib().lg_spread_tile_resource_topk_f64(
             N.ptr(A.by_user.rowptr[self.u0:]), N.ptr(A.by_user.col), N.ptr(scale.ra_edge),
             self.n, N.ptr(lines), N.ptr(ovf), A.n_items, N.ptr(scale.rb), N.ptr(inv_cls), int(j0),
             int(tile), int(width), N.ptr(self.eu), N.ptr(self.ei), self.d, N.ptr(gb), nch,
+            N.ptr(q), 0 if q is None else q.shape[1],
             N.ptr(ex.rowptr if ex is not None else None),
             N.ptr(ex.col if ex is not None else None), N.ptr(self.ex_cur), self.k,
             int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), N.stream_handle(self.dev)),
@@ -768,11 +784,12 @@ def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
     lambda), reusing what does not depend on lambda:
       dense  general_W (lg_spread_general_f64) once; per lambda W (lg_hybrid_weight_f64) and
              the fused F / top-k.
-      tiled  the general_W tiles (lambda-independent: ra / rb are applied by the walk) and
-             the score bounds are built once and cached on the device while they fit
-             ``cache_bytes`` (default: half the free memory); per lambda only the HybridScale
-             (ra per interaction, rb per item) changes. If the cache does not fit, each
-             lambda rebuilds the tiles.
+      tiled  the general_W tiles (lambda-independent: ra / rb are applied by the walk) are
+             built once and cached on the device while they fit ``cache_bytes`` (default:
+             half the free memory); per lambda only the HybridScale (ra per interaction, rb
+             per item) changes and the score bounds are recomputed (cheap; the per-column
+             bounds of every tile would not fit). If the cache does not fit, each lambda
+             rebuilds the tiles.
     Every result is bitwise the one spread_recommend(A, lam, ...) returns."""
     lams = [float(x) for x in lams]
     dev = A.k_item.device
@@ -798,21 +815,19 @@ def spread_lambda_sweep(A: Interactions, lams, k: int, excl: RowSets | None,
         scale = HybridScale(A, lam)
         walk.reset()
         if n > 0 and cached:
-            for (j0, width, lines, ovf, gb) in cache:
-                walk.step(lines, ovf, inv_cls, scale, j0, tile, width, j0 == 0, gb)
+            for (j0, width, lines, ovf) in cache:
+                walk.step(lines, ovf, inv_cls, scale, j0, tile, width, j0 == 0)
         else:
             tw = TileWeights(A, lam, tile)
             inv_cls = tw.inv_cls
             for j0 in range(0, I, tile):
                 tw.build(j0)
-                gb = walk.bounds(j0, tw.width)
-                walk.step(tw.lines, tw.ovf, inv_cls, scale, j0, tile, tw.width, j0 == 0, gb)
+                walk.step(tw.lines, tw.ovf, inv_cls, scale, j0, tile, tw.width, j0 == 0)
                 if n == 0 and cached and len(lams) > 1:
                     nov = (tw.n_units + 64) * 4
-                    need = tw.lines.numel() * 4 + nov * 4 + (gb.numel() * 4 if gb is not None else 0)
+                    need = tw.lines.numel() * 4 + nov * 4
                     if used + need <= cache_bytes:
-                        cache.append((j0, tw.width, tw.lines.clone(), tw.ovf[:nov].clone(),
-                                      None if gb is None else gb.clone()))
+                        cache.append((j0, tw.width, tw.lines.clone(), tw.ovf[:nov].clone()))
                         used += need
                     else:
                         cached = False

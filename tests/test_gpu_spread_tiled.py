@@ -375,3 +375,33 @@ def test_find_lambda_api_rows(tmp_path):
     assert list(df["lambda"]) == [0.0, 0.5, 1.0]
     assert df[["precision", "recall", "H", "I"]].notna().all().all()
     del pd
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_score_bounds_cover_chain_scores(d):
+    """lg_score_chunk_bound: the chunk bound gb and the per-column 8-bit bounds
+    gb * q / 255 are >= the exact fp32 chain score (the C chain of oracle/score_chain.c) of
+    every column, including a partial last chunk and users / items with large norms."""
+    from lgcnhs import ops
+    from oracle import lgcn_oracle as O
+    g = torch.Generator().manual_seed(d)
+    U, W, j0 = 70, 333, 40
+    eu = torch.randn(U, d, generator=g) * 0.1
+    ei = torch.randn(j0 + W + 5, d, generator=g) * 0.1
+    eu[3] *= 40.0
+    ei[j0 + 7] *= 25.0
+    ub, un = ops.bound_operands(eu.to(DEV))
+    ib, inn = ops.bound_operands(ei.to(DEV))
+    qs = -(-W // 256) * 256
+    q = torch.zeros((U, qs), dtype=torch.uint8, device=DEV)
+    gb, q = ops.chunk_bounds(ub, un, ib, inn, d, j0, W, qout=q)
+    G = O.chain_scores(eu.numpy(), ei[j0:j0 + W].numpy()).astype(np.float64)  # [U, W]
+    gbn = gb.cpu().numpy().astype(np.float64)
+    qn = q.cpu().numpy()[:, :W].astype(np.float64)
+    chunk = np.arange(W) // 64
+    assert np.all(gbn[:, chunk] >= G)
+    colb = gbn[:, chunk] * qn / 255.0
+    bad = colb < G
+    assert not bad.any(), (np.argwhere(bad)[:5], colb[bad][:5], G[bad][:5])
+    # and tight: the column bound is within a few % of the chunk bound's scale of the score
+    assert np.mean(colb - G) < np.mean(gbn[:, chunk] - G)
