@@ -439,6 +439,26 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     filled = float((idx >= 0).float().mean().item())
+    # roofline of the walk kernel (lg_spread_tile_resource_topk_f64), this rank, per launch:
+    # algorithmic bytes = the W-row bytes it must gather (one 128-B line per (user, item) and
+    # tile + overflow units: stats w_bytes) + 12 B of item id / ra per (user, item) + the
+    # user's list read and written (2 k 16 B) + its score bounds (qstride + 4 nch B) + 16 B of
+    # row pointers; time = HIP events around each launch on its stream
+    walk = None
+    if st.get("walk_launches"):
+        nl = st["walk_launches"]
+        per_user = 2 * k * 16 + st.get("qstride", 0) + 4 * st.get("nch", 0) + 16
+        alg = (st["w_bytes"] + 12 * st["user_items"] + per_user * st["users"] * nl) / nl
+        ms = st["t_walk_ms"] / nl
+        walk = {"bound": "hbm", "achieved": alg / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": alg / ms / 1e6 / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "lg_spread_tile_resource_topk_f64", "avg_launch_ms": ms,
+                "alg_bytes_per_launch": alg, "launches": nl,
+                "paths_per_launch": st["w_paths"] / nl,
+                "build_ms_per_tile": st["t_build_ms"] / nl,
+                "bounds_ms_per_tile": st["t_bounds_ms"] / nl,
+                "note": "latency / LDS-atomic bound (one ds_add_f64 per path); bytes are "
+                        "the W lines gathered, not a bandwidth limit"}
     evaluation = None
     try:
         evaluation = bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev)
@@ -449,7 +469,7 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
            "paths_per_s": paths / dt,
            "row_bytes_GBps": nbytes / dt / 1e9,
-           "tile": tile, "filled_frac_rank0": filled,
+           "tile": tile, "filled_frac_rank0": filled, "roofline": walk,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_tile_{seek,cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
                    "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64",

@@ -82,10 +82,33 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
       bfr[g][s] = *reinterpret_cast<const bf16x8 *>(ub + uu * D + 32 * s + 8 * kg);
     un[g] = unorm[uu];
   }
+  // q bytes of two chunks (64 users x 128 columns) staged in LDS, then written as whole
+  // 128-byte row segments (8 lanes x 16 bytes per user)
+  constexpr int QS = 36;  // dwords per user row: 32 + 4 (no bank conflicts, 16-B aligned)
+  __shared__ uint32_t qs_all[4][64 * QS];
+  uint32_t *qs = qs_all[threadIdx.x / 64];
+  // item fragments of a chunk: [tile t][k-step s]; the next chunk's are loaded while this
+  // chunk's MFMAs and bounds run
+  auto load_items = [&](int cb, bf16x8 (&fr)[4][S], float &nm) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      int it = cb + 16 * t + ul;  // A row = item
+      it = it < width ? it : width - 1;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        fr[t][s] = *reinterpret_cast<const bf16x8 *>(ib + (int64_t)(item_begin + it) * D +
+                                                     32 * s + 8 * kg);
+    }
+    nm = cb + lane < width ? inorm[item_begin + cb + lane] : 0.f;
+  };
+  bf16x8 fa[4][S], fb[4][S];
+  float na = 0.f, nb = 0.f;
+  load_items(0, fa, na);
   for (int c = 0; c < nch; ++c) {
     const int cb = 64 * c;  // chunk start inside the tile
+    if (c + 1 < nch) load_items(cb + 64, fb, nb);
     // the chunk's largest item norm (wave-uniform)
-    float inm = cb + lane < width ? inorm[item_begin + cb + lane] : 0.f;
+    float inm = na;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) inm = fmaxf(inm, __shfl_xor(inm, o));
     float gmax[4];
@@ -94,19 +117,12 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
     for (int g = 0; g < 4; ++g) gmax[g] = -__builtin_huge_valf();
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      int it = cb + 16 * t + ul;  // A row = item
-      it = it < width ? it : width - 1;
-      bf16x8 afr[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        afr[s] = *reinterpret_cast<const bf16x8 *>(ib + (int64_t)(item_begin + it) * D +
-                                                  32 * s + 8 * kg);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[s], bfr[g][s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][s], bfr[g][s], acc, 0, 0, 0);
         accs[t][g] = acc;
         // lane holds rows (items) 4*kg + r of this 16-item tile, column (user) ul
 #pragma unroll
@@ -136,12 +152,30 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
             const float qf = fminf(fmaxf(ceilf(v), 0.f), 255.f);
             w |= (uint32_t)qf << (8 * r);
           }
-          const int col = cb + 16 * t + 4 * kg;
-          if (uu < n_users && col < qstride)
-            *reinterpret_cast<uint32_t *>(qb + uu * qstride + col) = w;
+          // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair
+          qs[(16 * g + ul) * QS + (c & 1) * 16 + 4 * t + kg] = w;
         }
       }
     }
+    if (qb && ((c & 1) || c + 1 == nch)) {  // a chunk pair is complete: write it out
+      wave_sync();
+      const int cp = 64 * (c & ~1);  // the pair's first column
+#pragma unroll
+      for (int r8 = 0; r8 < 8; ++r8) {
+        const int uloc = 8 * r8 + (lane >> 3);
+        const int64_t uu = ubase + uloc;
+        const int col = cp + 16 * (lane & 7);
+        const uint4 v = *reinterpret_cast<const uint4 *>(qs + uloc * QS + 4 * (lane & 7));
+        if (uu < n_users && col + 16 <= qstride)
+          *reinterpret_cast<uint4 *>(qb + uu * qstride + col) = v;
+      }
+      wave_sync();
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < S; ++s) fa[t][s] = fb[t][s];
+    na = nb;
   }
 }
 

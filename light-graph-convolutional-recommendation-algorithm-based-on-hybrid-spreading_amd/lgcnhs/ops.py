@@ -613,9 +613,10 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     two-kernel form (F columns of a span of tiles written to a [users, span] scratch of
     ``scratch_bytes``, then lg_tile_topk_f64; the same F values, so the same lists).
     ``stats`` (optional dict) receives "w_paths": the paths the walk adds (sum over tiles and
-    users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the tile) and
+    users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the tile),
     "w_bytes": the row bytes it gathers (one 128-byte line per (user, item) and tile, plus
-    16 bytes per overflow unit)."""
+    16 bytes per overflow unit) and, on the fused path, the HIP-event times of the tile
+    builds / score bounds / walk launches (t_*_ms, walk_launches)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -641,11 +642,33 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
         tw.bytes_read = torch.zeros((), dtype=torch.int64, device=dev)
     if fused:
         walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile)
+        evs = [] if stats is not None else None
         for j0 in range(i0, i1, tile):
+            if evs is not None:  # per-tile HIP events on the launch stream: build / bounds / walk
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                e[0].record()
             tw.build(j0, stop=i1)
-            walk.step(tw.lines, tw.ovf, tw.inv_cls, tw.scale, j0, tile, tw.width, j0 == i0)
+            if evs is not None:
+                e[1].record()
+            bnd = walk.bounds(j0, tw.width)
+            if evs is not None:
+                e[2].record()
+            walk.step(tw.lines, tw.ovf, tw.inv_cls, tw.scale, j0, tile, tw.width, j0 == i0, bnd)
+            if evs is not None:
+                e[3].record()
+                evs.append(e)
         vals.copy_(walk.vals)
         idxs.copy_(walk.idxs)
+        if evs:
+            torch.cuda.synchronize(dev)
+            stats["t_build_ms"] = stats.get("t_build_ms", 0.0) + sum(e[0].elapsed_time(e[1]) for e in evs)
+            stats["t_bounds_ms"] = stats.get("t_bounds_ms", 0.0) + sum(e[1].elapsed_time(e[2]) for e in evs)
+            stats["t_walk_ms"] = stats.get("t_walk_ms", 0.0) + sum(e[2].elapsed_time(e[3]) for e in evs)
+            stats["walk_launches"] = stats.get("walk_launches", 0) + len(evs)
+            stats["user_items"] = stats.get("user_items", 0) + int(tw.row_uses.sum()) * len(evs)
+            stats["users"] = n
+            stats["qstride"] = 0 if walk.d == 0 or walk.qbuf is None else walk.qbuf.shape[1]
+            stats["nch"] = -(-tile // 64) if walk.d else 0
     else:
         span = max(tile, scratch_bytes // (n * 8) // tile * tile)
         span = min(span, -(-(i1 - i0) // tile) * tile)

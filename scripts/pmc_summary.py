@@ -69,11 +69,15 @@ def main(out_dir, tag, workload="c5-d64", world=1):
     tp = os.path.join(out_dir, "pmc_traffic.json")
     d = json.load(open(tp)) if os.path.exists(tp) else {}
     if "lg_spmm_layer_f32" in stats and "hbm_bytes_per_launch" in stats["lg_spmm_layer_f32"]:
+        import hashlib  # the kernel source the counters were measured on (bench.py checks it)
+        src = os.path.join(REPO, "light-graph-convolutional-recommendation-algorithm-based-on-"
+                           "hybrid-spreading_amd", "csrc", "spmm.hip")
+        sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
         d[f"{workload}/n{world}"] = {"kernel": "lg_spmm_layer_f32", "source": tag,
-                                     **stats["lg_spmm_layer_f32"]}
+                                     "kernel_sha": sha, **stats["lg_spmm_layer_f32"]}
     json.dump(d, open(tp, "w"), indent=1)
     print(json.dumps(stats, indent=1))
 
 
 if __name__ == "__main__":
-    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r02")

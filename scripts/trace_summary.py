@@ -12,7 +12,12 @@ from collections import defaultdict
 
 def short(name):
     m = re.search(r"(lg::[A-Za-z_0-9]+(<[^>]*>)?)", name)
-    return m.group(1) if m else None
+    if m:
+        return m.group(1)
+    m = re.search(r"_ZN2lg(\d+)([A-Za-z_0-9]+)", name)  # names the tracer left mangled
+    if m:
+        return "lg::" + m.group(2)[:int(m.group(1))]
+    return None
 
 
 def main(trace_dir, stem, command=""):
