@@ -414,7 +414,7 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     lists of its user block. Timed end to end (max over ranks). Also the Douban-shaped dense
     path (configs[2]: SpreadLightGCNOpti, lam=0.5) at N=1."""
     from lgcnhs import ops
-    from lgcnhs.dist import sharded_spread_topk
+    from lgcnhs.dist import item_range, sharded_spread_topk
     from lgcnhs.synth import synth_interactions
     A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
     eu = e0_orig[:U].contiguous()
@@ -429,7 +429,10 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
                                            stats=st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    paths, nbytes = float(st.get("w_paths", 0)), float(st.get("w_bytes", 0))
+    # the walk's paths / row bytes: counted from the tiles after the timed run (untimed)
+    i0, i1 = item_range(I, tile, rank, world)
+    st["w_paths"], st["w_bytes"] = ops.tile_traffic(A, tile, items=slice(i0, i1))
+    paths, nbytes = float(st["w_paths"]), float(st["w_bytes"])
     if world > 1:
         e = torch.tensor([paths, nbytes], dtype=torch.float64, device=dev)
         dist.all_reduce(e)
@@ -471,7 +474,7 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
            "row_bytes_GBps": nbytes / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled, "roofline": walk,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
-           "path": "lg_spread_tile_{seek,cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
+           "path": "lg_spread_group_{cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
                    "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64",
            "eval": evaluation}
     if world == 1:

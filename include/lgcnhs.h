@@ -276,6 +276,37 @@ int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_user
                             void *lines, void *ovf, int32_t *row_len, void *ws,
                             size_t ws_bytes, lg_stream_t stream);
 
+/* Group build: the three calls above for n_tiles (<= 8) consecutive tiles at once, each
+ * (item row, user) pair visited once per group instead of once per tile. Tile t of the group
+ * is [group_begin + t tile, min(group_begin + (t + 1) tile, stop)).
+ * lg_spread_group_cursor: counts[v][0..7] (8 uint16 per user, 16-byte aligned, unused
+ *   tiles 0) = user v's items in each tile, end[v] = the position after the group's last
+ *   (cur[v] = the first position with item >= group_begin; cur and end must not alias).
+ * lg_spread_group_bound: bound[t][i] ([n_tiles][n_items] int64) = lg_spread_tile_bound of
+ *   tile t.
+ * lg_spread_group_rows_f64: lg_spread_tile_rows_f64 of every tile t of the group, tile t's
+ *   lines at lines + t (n_items + 1) 128 bytes (each tile's line n_items zeroed by the
+ *   caller), its overflow runs at ovf + 16 ovf_base[t] bytes (ovf_base: device int64
+ *   [n_tiles], in 16-byte units), ovf_ptr / row_len as [n_tiles][n_items] with the per-tile
+ *   meaning of lg_spread_tile_rows_f64 (the same words bit for bit); vthr in [31, 65535];
+ *   ws: lg_spread_group_rows_ws_bytes(n_items, n_tiles) bytes. */
+int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
+                           int64_t n_users, int32_t group_begin, int32_t tile, int32_t n_tiles,
+                           int32_t stop, const int64_t *cur, int64_t *end, uint16_t *counts,
+                           lg_stream_t stream);
+int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *item_users,
+                          int64_t n_items, const uint16_t *counts, int32_t n_tiles,
+                          int64_t *bound, lg_stream_t stream);
+size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles);
+int lg_spread_group_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                             const int32_t *user_items, const uint16_t *user_cls,
+                             const double *inv_deg, int64_t n_items, const int64_t *cur,
+                             const uint16_t *counts, int32_t group_begin, int32_t tile,
+                             int32_t n_tiles, const int64_t *bound, int64_t vthr,
+                             const int64_t *ovf_ptr, const int64_t *ovf_base, void *lines,
+                             void *ovf, int32_t *row_len, void *ws, size_t ws_bytes,
+                             lg_stream_t stream);
+
 /* F[u][j - item_begin] = rb[j] * sum over the paths of u's items of the tile's rows (see the
  * section comment) for the n_users rows of user_rowptr (pass user_rowptr + u0 for a block)
  * and j in [item_begin, item_begin + tile) (columns >= item_begin + width are 0); F

@@ -26,6 +26,7 @@ namespace lg {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBoundMargin = 0.008f;
 
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(256) void k_bound_prep(const float *__restrict__ x,
 
 // One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile.
 template <int D>
-__global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ ub,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_chunk_bound(const __bf16 *__restrict__ ub,
                                                      const float *__restrict__ unorm,
                                                      int64_t n_users,
                                                      const __bf16 *__restrict__ ib,
@@ -114,8 +115,6 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
     float gmax[4];
     f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
-    for (int g = 0; g < 4; ++g) gmax[g] = -__builtin_huge_valf();
-#pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -124,11 +123,27 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
         for (int s = 0; s < S; ++s)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][s], bfr[g][s], acc, 0, 0, 0);
         accs[t][g] = acc;
-        // lane holds rows (items) 4*kg + r of this 16-item tile, column (user) ul
+      }
+    }
+    // lane holds rows (items) 4 kg + r of each 16-item tile, column (user) ul; columns past
+    // the width (a partial last chunk only) do not count
+    if (cb + 64 > width) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (cb + 16 * t + 4 * kg + r < width) gmax[g] = fmaxf(gmax[g], acc[r]);
-      }
+          if (cb + 16 * t + 4 * kg + r >= width)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) accs[t][g][r] = -__builtin_huge_valf();
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float m = fmaxf(fmaxf(accs[0][g][0], accs[0][g][1]), fmaxf(accs[0][g][2], accs[0][g][3]));
+#pragma unroll
+      for (int t = 1; t < 4; ++t)
+        m = fmaxf(fmaxf(m, fmaxf(accs[t][g][0], accs[t][g][1])),
+                  fmaxf(accs[t][g][2], accs[t][g][3]));
+      gmax[g] = m;
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -141,17 +156,22 @@ __global__ __launch_bounds__(256) void k_chunk_bound(const __bf16 *__restrict__ 
       const int64_t uu = ubase + 16 * g + ul;
       if (kg == 0 && uu < n_users) gb[uu * nch + c] = b;
       if (qb) {
-        // per column: 4 consecutive items of one user per lane and tile -> one dword
-        const float sc = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) : 0.f;
+        // per column: q = ceil(v), v = fl(acc sc + msc) >= 255 (acc + marg) / b (sc and msc
+        // carry (1 + 2^-20) factors over their own roundings and the fma's), clamped to
+        // [0, 255]; 4 consecutive items of one user per lane and tile -> one dword
+        const float sc = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) * (1.f + 0x1p-20f) : 0.f;
+        const float msc = marg * sc * (1.f + 0x1p-20f);
+        const f32x2 sc2 = {sc, sc}, ms2 = {msc, msc};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
+          const f32x2 lo = __builtin_elementwise_fma(f32x2{accs[t][g][0], accs[t][g][1]}, sc2, ms2);
+          const f32x2 hi = __builtin_elementwise_fma(f32x2{accs[t][g][2], accs[t][g][3]}, sc2, ms2);
+          const float v[4] = {lo[0], lo[1], hi[0], hi[1]};
           uint32_t w = 0;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = (accs[t][g][r] + marg) * sc * (1.f + 0x1p-20f);
-            const float qf = fminf(fmaxf(ceilf(v), 0.f), 255.f);
-            w |= (uint32_t)qf << (8 * r);
-          }
+          for (int r = 0; r < 4; ++r)
+            w = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_ceilf(__builtin_amdgcn_fmed3f(v[r], 0.f, 255.f)), r, w);
           // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair
           qs[(16 * g + ul) * QS + (c & 1) * 16 + 4 * t + kg] = w;
         }

@@ -302,6 +302,260 @@ __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ bo
   if (bound[i] > vthr) hub_rows[atomicAdd(n_hub, 1ull)] = i;
 }
 
+// ------------------------------------------------------------ group build (S tiles at once)
+// The per-tile passes above visit every (item row, user) pair once per TILE, although at C5
+// a user has ~0.2 items in a 2048-column tile: 489 tiles x 1e8 visits of gathered counts.
+// The group passes visit each pair once per GROUP of up to kGroupMax consecutive tiles and
+// write the group's tiles together (tile t of the group at lines + t (n_items + 1) 32 words,
+// its overflow runs at ovf + 4 ovf_base[t] words). Every word equals the per-tile build's
+// (same slot order, same headers; the caller places the runs with the same exclusive prefix).
+constexpr int kGroupMax = 8;
+
+// counts[v][t] (kGroupMax uint16 per user) = the items of user v in tile t of the group
+// ([group_begin + t tile, min(group_begin + (t + 1) tile, stop))), end[v] = the position
+// after the group's last; cur[v] = the first position with item >= group_begin.
+__global__ __launch_bounds__(256) void k_group_cursor(const int64_t *__restrict__ user_rowptr,
+                                                      const int32_t *__restrict__ user_items,
+                                                      int64_t n_users, int32_t group_begin,
+                                                      int32_t tile, int32_t n_tiles,
+                                                      int32_t stop, const int64_t *__restrict__ cur,
+                                                      int64_t *__restrict__ end,
+                                                      uint4 *__restrict__ counts) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_users) return;
+  int64_t p = cur[v];
+  const int64_t pe = user_rowptr[v + 1];
+  uint32_t c[kGroupMax];
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t) {
+    c[t] = 0;
+    if (t < n_tiles) {
+      const int64_t l = (int64_t)group_begin + (int64_t)(t + 1) * tile;
+      const int32_t lim = (int32_t)(l < stop ? l : stop);
+      const int64_t p0 = p;
+      while (p < pe && user_items[p] < lim) ++p;
+      c[t] = (uint32_t)(p - p0);  // <= tile <= 8192
+    }
+  }
+  end[v] = p;
+  counts[v] = uint4{c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16};
+}
+
+__device__ __forceinline__ uint32_t count_of(const uint4 &c, int t) {
+  const uint32_t w = t < 2 ? c.x : (t < 4 ? c.y : (t < 6 ? c.z : c.w));
+  return (t & 1) ? w >> 16 : w & 0xFFFFu;
+}
+
+// bound[t][i] = sum over the users v of item i of counts[v][t] (the pairs behind row i in
+// tile t). One wave per item row.
+__global__ __launch_bounds__(256) void k_group_bound(const int64_t *__restrict__ item_rowptr,
+                                                     const int32_t *__restrict__ item_users,
+                                                     int64_t n_items,
+                                                     const uint4 *__restrict__ counts,
+                                                     int32_t n_tiles, int64_t *__restrict__ bound) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (i >= n_items) return;
+  const int lane = lane_id();
+  int64_t s[kGroupMax];
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t) s[t] = 0;
+  for (int64_t e = item_rowptr[i] + lane; e < item_rowptr[i + 1]; e += 64) {
+    const uint4 c = counts[item_users[e]];
+#pragma unroll
+    for (int t = 0; t < kGroupMax; ++t) s[t] += count_of(c, t);
+  }
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t) {
+    if (t < n_tiles) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s[t] += __shfl_xor(s[t], o);
+      if (lane == 0) bound[(int64_t)t * n_items + i] = s[t];
+    }
+  }
+}
+
+// P rows of every tile of the group: one wave per item row (tiles whose row is a hub row,
+// bound > vthr, are left to k_group_rows_hub). The lanes' counts of two tiles are scanned
+// together as 16-bit fields of one word: a P row's prefix never exceeds its bound <= vthr <
+// 2^16, and hub tiles' counts are masked to 0 before the scan.
+__global__ __launch_bounds__(256) void k_group_rows(
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int32_t *__restrict__ user_items, const uint16_t *__restrict__ user_cls,
+    int64_t n_items, const int64_t *__restrict__ cur, const uint4 *__restrict__ counts,
+    int32_t group_begin, int32_t tile, int32_t n_tiles, const int64_t *__restrict__ bound,
+    int64_t vthr, const int64_t *__restrict__ ovf_ptr, const int64_t *__restrict__ ovf_base,
+    uint32_t *__restrict__ lines, uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (i >= n_items) return;
+  const int lane = lane_id();
+  const int64_t nbl = lane < n_tiles ? bound[(int64_t)lane * n_items + i] : 0;
+  const int64_t oul = lane < n_tiles ? ovf_ptr[(int64_t)lane * n_items + i] : 0;
+  const int64_t obl = lane < n_tiles ? ovf_base[lane] : 0;
+  const int64_t tstride = (n_items + 1) * 32;  // words per tile of lines
+  // P tiles of this row (wave-uniform)
+  const uint32_t pmask = (uint32_t)__ballot(lane < n_tiles && nbl <= vthr);
+  for (int t = 0; t < n_tiles; ++t) {
+    if (!((pmask >> t) & 1)) continue;
+    const int64_t nb = __shfl(nbl, t);
+    const bool has_ovf = nb > kLineSlots;
+    const int64_t ou = has_ovf ? __shfl(oul, t) : 0;
+    uint32_t *line = lines + (int64_t)t * tstride + i * 32;
+    uint32_t *ov = ovf + __shfl(obl, t) * 4;
+    const int64_t n_units = has_ovf ? (nb - kLineSlots + 3) / 4 : 0;
+    const int64_t cap = kLineSlots + 4 * n_units;
+    if (has_ovf && lane < 4) ov[ou * 4 + lane] = lane == 0 ? (uint32_t)n_units : 0u;
+    for (int64_t p = nb + lane; p < cap; p += 64) put_slot(line, ov, ou, p, 0u);
+  }
+  int64_t n[kGroupMax];
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t) n[t] = 0;
+  uint32_t farbits = 0;
+  const int64_t e1 = item_rowptr[i + 1];
+  for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
+    const int64_t e = e0 + lane;
+    uint4 c4{0u, 0u, 0u, 0u};
+    int32_t v = 0;
+    if (e < e1) {
+      v = item_users[e];
+      c4 = counts[v];
+    }
+    // hub tiles' counts masked out (their items still advance the lane's offset)
+    uint32_t m4[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint32_t lo = ((pmask >> (2 * h)) & 1) ? 0xFFFFu : 0u;
+      const uint32_t hi = ((pmask >> (2 * h + 1)) & 1) ? 0xFFFF0000u : 0u;
+      m4[h] = lo | hi;
+    }
+    const uint32_t w[4] = {c4.x & m4[0], c4.y & m4[1], c4.z & m4[2], c4.w & m4[3]};
+    if (__ballot((w[0] | w[1] | w[2] | w[3]) != 0) == 0) continue;  // no pair in any P tile
+    int64_t s0 = 0;
+    uint32_t cl = 0;
+    if ((c4.x | c4.y | c4.z | c4.w) != 0) {
+      s0 = cur[v];
+      cl = (uint32_t)user_cls[v];
+    }
+    uint32_t off = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      if (2 * h >= n_tiles) break;
+      uint32_t pre = w[h];
+      if (__ballot(pre != 0) != 0) {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(pre, o);
+          if (lane >= o) pre += y;
+        }
+      }
+      const uint32_t total = __shfl(pre, 63);
+      pre -= w[h];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int t = 2 * h + b;
+        const uint32_t ct = (w[h] >> (16 * b)) & 0xFFFFu;
+        const uint32_t tot = (total >> (16 * b)) & 0xFFFFu;
+        if (tot) {
+          const uint32_t pb = (pre >> (16 * b)) & 0xFFFFu;
+          uint32_t *line = lines + (int64_t)t * tstride + i * 32;
+          uint32_t *ov = ovf + __shfl(obl, t) * 4;
+          const int64_t ou = __shfl(oul, t);
+          const int32_t ib = group_begin + t * tile;
+          for (uint32_t q = 0; q < ct; ++q)
+            put_slot(line, ov, ou, n[t] + pb + q,
+                     (cl << 16) | (uint32_t)(user_items[s0 + off + q] - ib));
+          if (ct && cl >= (uint32_t)kInvTab) farbits |= 1u << t;
+          n[t] += tot;
+        }
+        off += count_of(c4, t);
+      }
+    }
+  }
+  for (int t = 0; t < n_tiles; ++t) {
+    if (!((pmask >> t) & 1)) continue;
+    const bool slow = __ballot((farbits >> t) & 1) != 0;
+    const int64_t nb = __shfl(nbl, t);
+    const bool has_ovf = nb > kLineSlots;
+    const int64_t ou = __shfl(oul, t);
+    if (lane == 0) {
+      lines[(int64_t)t * tstride + i * 32] =
+          (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u) | (slow ? kHdrSlow : 0u);
+      if (row_len) row_len[(int64_t)t * n_items + i] = (int32_t)nb;
+    }
+  }
+}
+
+// Hub rows of the group (flat index t * n_items + i of rows with bound > vthr, listed by
+// k_hub_list over the [n_tiles][n_items] bounds): k_tile_rows_hub's block-wide dense LDS
+// accumulation, on tile t's cursor cur[v] + (v's items in tiles < t).
+__global__ __launch_bounds__(256) void k_group_rows_hub(
+    const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
+    int64_t n_items, const int64_t *__restrict__ cur, const uint4 *__restrict__ counts,
+    int32_t group_begin, int32_t tile, const int64_t *__restrict__ ovf_ptr,
+    const int64_t *__restrict__ ovf_base, uint32_t *__restrict__ lines,
+    uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
+  extern __shared__ double acc[];  // tile doubles
+  __shared__ int wsum[4];
+  const int64_t nh = *n_hub;
+  for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int64_t flat = hub_rows[h];
+    const int t = (int)(flat / n_items);
+    const int64_t i = flat - (int64_t)t * n_items;
+    const int32_t item_begin = group_begin + t * tile;
+    for (int j = threadIdx.x; j < tile; j += blockDim.x) acc[j] = 0.0;
+    __syncthreads();
+    for (int64_t e = item_rowptr[i]; e < item_rowptr[i + 1]; ++e) {
+      const int32_t v = item_users[e];
+      const uint4 c4 = counts[v];
+      const int c = (int)count_of(c4, t);
+      if (c == 0) continue;  // uniform across the block: no barrier skipped unevenly
+      int64_t s0 = cur[v];
+      for (int q = 0; q < t; ++q) s0 += count_of(c4, q);
+      const double wv = inv_deg[v];
+      for (int q = threadIdx.x; q < c; q += blockDim.x) acc[user_items[s0 + q] - item_begin] += wv;
+      __syncthreads();  // the next user may hit the same columns from other threads
+    }
+    uint32_t *line = lines + (int64_t)t * (n_items + 1) * 32 + i * 32;
+    uint32_t *ov = ovf + ovf_base[t] * 4;
+    const int64_t ou = ovf_ptr[flat];
+    int base = 0;
+    for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
+      const int j = j0 + threadIdx.x;
+      const bool nz = j < tile && acc[j] != 0.0;
+      const uint64_t b = __ballot(nz);
+      const int w = threadIdx.x / 64;
+      if (lane_id() == 0) wsum[w] = __popcll(b);
+      __syncthreads();
+      int before_w = 0, total = 0;
+      for (int q = 0; q < 4; ++q) {
+        if (q < w) before_w += wsum[q];
+        total += wsum[q];
+      }
+      if (nz) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(acc[j]);
+        const int64_t e = base + before_w + __popcll(b & lanemask_lt());
+        uint32_t *u4 = e < kLineEnts ? line + 4 * (1 + e) : ov + 4 * (ou + 1 + (e - kLineEnts));
+        *reinterpret_cast<uint4 *>(u4) =
+            uint4{kEntV | (uint32_t)j, (uint32_t)bits, (uint32_t)(bits >> 32), 0u};
+      }
+      base += total;
+      __syncthreads();
+    }
+    const bool has_ovf = base > kLineEnts;
+    if (threadIdx.x < 32) {
+      const int tw = threadIdx.x;  // line word
+      const int unit = tw / 4;
+      if (tw == 0) line[0] = kHdrV | kHdrSlow | (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u);
+      else if (unit == 0 || unit > base) line[tw] = 0u;
+    }
+    if (has_ovf && threadIdx.x < 4)
+      ov[ou * 4 + threadIdx.x] = threadIdx.x == 0 ? (uint32_t)(base - kLineEnts) : 0u;
+    if (threadIdx.x == 0 && row_len) row_len[flat] = base;
+    __syncthreads();
+  }
+}
+
 template <int Q>
 __device__ __forceinline__ void load_frag(const float *__restrict__ p, float (&v)[Q]) {
   const float4 *p4 = reinterpret_cast<const float4 *>(p);
@@ -672,6 +926,12 @@ constexpr int MODE_F = 0, MODE_TOPK = 1;
 constexpr int kWalkQ = 8;       // line loads per lane per batch: 8 rows each, 64 rows
 constexpr int kBatchRows = 8 * kWalkQ;
 constexpr int kOvfList = kBatchRows;
+#ifndef LG_DECODE_PHASE
+#define LG_DECODE_PHASE 4
+#endif
+constexpr int kDecodePhase = LG_DECODE_PHASE;
+  // lines whose class reads precede their adds
+static_assert(kWalkQ % kDecodePhase == 0, "decode phase must divide the batch's line loads");
 
 struct WalkArgs {
   const int64_t *user_rowptr;
@@ -713,7 +973,8 @@ __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
          ~(size_t)15;
 }
 __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
-  return (size_t)kInvTab * 8 + 16 * 8;  // class table + the block's rb maxima
+  // class table + the block's rb maxima + rb of the tile's columns
+  return (size_t)kInvTab * 8 + 16 * 8 + (size_t)tile * 8;
 }
 
 __device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
@@ -779,7 +1040,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   const int tile = a.tile;
   double *s_inv = lds;  // at LDS address 0 (the fast decode indexes it with class * 8)
   double *s_red = s_inv + kInvTab;
-  char *mine = reinterpret_cast<char *>(s_red + 16) +
+  double *s_rb = s_red + 16;  // rb of the tile's columns (0 past the width)
+  char *mine = reinterpret_cast<char *>(s_rb + tile) +
                (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
   double *ovl_ra = acc + tile;  // overflow list (decode)
@@ -789,7 +1051,11 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 
   for (int c = threadIdx.x; c < kInvTab; c += blockDim.x) s_inv[c] = a.g_inv[c];
   double rmax = 0.0;  // the tile's largest rb (top-K prefilter)
-  for (int j = threadIdx.x; j < a.width; j += blockDim.x) rmax = fmax(rmax, a.rbeta[a.item_begin + j]);
+  for (int j = threadIdx.x; j < tile; j += blockDim.x) {
+    const double rb = j < a.width ? a.rbeta[a.item_begin + j] : 0.0;
+    s_rb[j] = rb;
+    rmax = fmax(rmax, rb);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, o));
   if (lane == 0) s_red[wave] = rmax;
@@ -924,12 +1190,27 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     const bool slow = __ballot(hdr & kHdrSlow) != 0;
     const bool ovf = __ballot(hdr & kHdrOvf) != 0;
     if (!slow) {
+      // The LDS serves a wave's operations in order, so a class-table read issued after an
+      // atomic returns only once the atomic is done: the reads of H lines' slots go out
+      // first, then their adds (one wait per phase, not one per slot).
+      constexpr int H = kDecodePhase;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        add_slot_fast(acc, w[q].x & hmask, ra[q], s_inv);
-        add_slot_fast(acc, w[q].y, ra[q], s_inv);
-        add_slot_fast(acc, w[q].z, ra[q], s_inv);
-        add_slot_fast(acc, w[q].w, ra[q], s_inv);
+      for (int q0 = 0; q0 < Q; q0 += H) {
+        double inv[H][4];
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          inv[q][0] = s_inv[(w[q0 + q].x & hmask) >> 16];
+          inv[q][1] = s_inv[w[q0 + q].y >> 16];
+          inv[q][2] = s_inv[w[q0 + q].z >> 16];
+          inv[q][3] = s_inv[w[q0 + q].w >> 16];
+        }
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          const uint32_t sv[4] = {w[q0 + q].x & hmask, w[q0 + q].y, w[q0 + q].z, w[q0 + q].w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (sv[t]) lds_add(acc, sv[t] & 0xFFFFu, inv[q][t] * ra[q0 + q]);
+        }
       }
     } else {
 #pragma unroll
@@ -987,8 +1268,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     if constexpr (MODE == MODE_F) {
       double *row = a.F + u * a.ldf;
       for (int j = lane; j < tile; j += 64) {
-        const double rb = j < a.width ? a.rbeta[a.item_begin + (j < a.width ? j : 0)] : 0.0;
-        __builtin_nontemporal_store(acc[j] * rb, row + j);
+        __builtin_nontemporal_store(acc[j] * s_rb[j], row + j);
         acc[j] = 0.0;
       }
     } else {
@@ -1144,7 +1424,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #pragma unroll
           for (int x = 1; x < 8; ++x) s = t == x ? sv[x] : s;
           const int j = c0 + 256 * (t >> 2) + 4 * lane + (t & 3);
-          const double f = has ? s * a.rbeta[a.item_begin + (has ? j : 0)] : -1.0;
+          const double f = has ? s * s_rb[has ? j : 0] : -1.0;
           if constexpr (D > 0) {
             const uint32_t qq = t < 4 ? qa : qb2;
             const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
@@ -1458,6 +1738,79 @@ extern "C" int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t
       hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, cur, count, item_begin, tile,
       ovf_ptr, (uint32_t *)lines, (uint32_t *)ovf, row_len);
   return launch_status("lg_spread_tile_rows_f64");
+}
+
+extern "C" int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
+                                      int64_t n_users, int32_t group_begin, int32_t tile,
+                                      int32_t n_tiles, int32_t stop, const int64_t *cur,
+                                      int64_t *end, uint16_t *counts, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && cur && end && counts && n_users >= 0 && cur != end &&
+                 group_begin >= 0 && stop > group_begin,
+             "lg_spread_group_cursor: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
+             "lg_spread_group_cursor: tile %d / n_tiles %d", tile, n_tiles);
+  LG_REQUIRE(((uintptr_t)counts & 15) == 0, "lg_spread_group_cursor: counts not 16-byte aligned");
+  if (n_users == 0) return LG_OK;
+  k_group_cursor<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0,
+                   (hipStream_t)stream>>>(user_rowptr, user_items, n_users, group_begin, tile,
+                                          n_tiles, stop, cur, end, (uint4 *)counts);
+  return launch_status("lg_spread_group_cursor");
+}
+
+extern "C" int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *item_users,
+                                     int64_t n_items, const uint16_t *counts, int32_t n_tiles,
+                                     int64_t *bound, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && counts && bound && n_items >= 0 && n_tiles >= 1 &&
+                 n_tiles <= kGroupMax && ((uintptr_t)counts & 15) == 0,
+             "lg_spread_group_bound: bad arguments");
+  if (n_items == 0) return LG_OK;
+  k_group_bound<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
+      item_rowptr, item_users, n_items, (const uint4 *)counts, n_tiles, bound);
+  return launch_status("lg_spread_group_bound");
+}
+
+extern "C" size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles) {
+  return (size_t)(n_items * (n_tiles > 0 ? n_tiles : 1) + 1) * sizeof(int64_t);
+}
+
+extern "C" int lg_spread_group_rows_f64(
+    const int64_t *item_rowptr, const int32_t *item_users, const int32_t *user_items,
+    const uint16_t *user_cls, const double *inv_deg, int64_t n_items, const int64_t *cur,
+    const uint16_t *counts, int32_t group_begin, int32_t tile, int32_t n_tiles,
+    const int64_t *bound, int64_t vthr, const int64_t *ovf_ptr, const int64_t *ovf_base,
+    void *lines, void *ovf, int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && counts && bound && ovf_ptr &&
+                 ovf_base && lines && ovf && n_items >= 0 && group_begin >= 0,
+             "lg_spread_group_rows_f64: bad arguments");
+  LG_REQUIRE(vthr >= kLineSlots && vthr < 65536,
+             "lg_spread_group_rows_f64: vthr %lld not in [31, 65535]", (long long)vthr);
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
+             "lg_spread_group_rows_f64: tile %d / n_tiles %d", tile, n_tiles);
+  LG_REQUIRE(((uintptr_t)counts & 15) == 0, "lg_spread_group_rows_f64: counts not 16-byte aligned");
+  if (n_items == 0) return LG_OK;
+  const size_t need = lg_spread_group_rows_ws_bytes(n_items, n_tiles);
+  if (!ws || ws_bytes < need) {
+    set_error("lg_spread_group_rows_f64: workspace %zu < %zu bytes", ws_bytes, need);
+    return LG_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *n_hub = (int64_t *)ws;
+  int64_t *hub_rows = n_hub + 1;
+  if (hipMemsetAsync(n_hub, 0, sizeof(int64_t), s) != hipSuccess) {
+    set_error("lg_spread_group_rows_f64: hipMemsetAsync failed");
+    return LG_ERR_HIP;
+  }
+  const uint4 *c4 = (const uint4 *)counts;
+  k_group_rows<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, s>>>(
+      item_rowptr, item_users, user_items, user_cls, n_items, cur, c4, group_begin, tile, n_tiles,
+      bound, vthr, ovf_ptr, ovf_base, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+  const int64_t nflat = n_items * n_tiles;
+  k_hub_list<<<dim3((unsigned)((nflat + 255) / 256)), dim3(256), 0, s>>>(
+      bound, nflat, vthr, (unsigned long long *)n_hub, hub_rows);
+  k_group_rows_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
+      hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, n_items, cur, c4,
+      group_begin, tile, ovf_ptr, ovf_base, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+  return launch_status("lg_spread_group_rows_f64");
 }
 
 static int walk_dbg() {  // measurement knob only: results are wrong when set

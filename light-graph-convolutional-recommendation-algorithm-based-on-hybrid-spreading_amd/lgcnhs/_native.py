@@ -18,6 +18,8 @@ import torch  # noqa: F401  (must be imported before the library: shared HIP run
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "liblgcnhs.so")
+# measurement builds (scripts/ab_*): another build of the same library
+LIB_PATH = os.environ.get("LGCNHS_LIB_PATH") or LIB_PATH
 
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
@@ -78,6 +80,15 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp,
          _vp, _sz, _vp],
+    ),
+    "lg_spread_group_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp,
+                                              _vp, _vp]),
+    "lg_spread_group_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _vp, _vp]),
+    "lg_spread_group_rows_ws_bytes": (_sz, [_i64, _i32]),
+    "lg_spread_group_rows_f64": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp,
+         _vp, _vp, _vp, _sz, _vp],
     ),
     "lg_spread_tile_resource_f64": (
         ctypes.c_int,

@@ -413,9 +413,16 @@ class TileWeights:
     general_W values of hub items). The tile itself is lambda-independent; ``lam`` sets the
     HybridScale that resource() applies. build() moves to the next tile; the buffers are
     reused and grown on demand. ``vthr``: rows with more pairs are V rows (default: the tile
-    width; LGCNHS_V_THRESHOLD overrides)."""
+    width; LGCNHS_V_THRESHOLD overrides).
 
-    def __init__(self, A: Interactions, lam: float, tile: int, vthr: int | None = None):
+    Tiles are built ``group`` at a time (default 8, LGCNHS_TILE_GROUP; 1 = the per-tile
+    passes lg_spread_tile_cursor / _bound / _rows_f64): lg_spread_group_cursor / _bound /
+    _rows_f64 visit each (item row, user) pair once per group instead of once per tile and
+    write the group's tiles side by side; build(j0) of a tile inside the built group only
+    selects it. Either way every tile's words are the same bit for bit."""
+
+    def __init__(self, A: Interactions, lam: float, tile: int, vthr: int | None = None,
+                 group: int | None = None):
         if not 1 <= tile <= 8192:
             raise ValueError(f"tile {tile} not in [1, 8192]")
         self.A, self.tile, self.lam = A, int(tile), float(lam)
@@ -424,25 +431,38 @@ class TileWeights:
         if vthr is None:
             vthr = int(os.environ.get("LGCNHS_V_THRESHOLD", "0")) or self.tile
         self.vthr = max(LINE_SLOTS, int(vthr))
+        if group is None:
+            group = int(os.environ.get("LGCNHS_TILE_GROUP", "8"))
+        if not 1 <= group <= 8:
+            raise ValueError(f"group {group} not in [1, 8]")
+        if group > 1 and self.vthr > 65535:
+            raise ValueError(f"vthr {self.vthr} > 65535 needs group=1")
         I = A.n_items
+        self.group = int(min(group, max(1, -(-I // self.tile))))
+        S = self.group
         self.cur = A.by_user.rowptr[:-1].contiguous().clone()
         self.end = torch.empty_like(self.cur)
-        self.count = torch.empty(A.n_users, dtype=torch.uint16, device=dev)
+        if S == 1:
+            self.counts = torch.empty(A.n_users, dtype=torch.uint16, device=dev)
+        else:  # 8 uint16 per user (one 16-byte load)
+            self.counts = torch.empty((A.n_users, 8), dtype=torch.uint16, device=dev)
         self.inv_deg = torch.empty(A.n_users, dtype=torch.float64, device=dev)
         N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,
                                           N.ptr(self.inv_deg), N.stream_handle(dev)),
                 "lg_inv_degree_f64")
         self.user_cls, self.inv_cls = degree_classes(A.by_user.degrees())
-        self.bound = torch.empty(I, dtype=torch.int64, device=dev)
-        self.ovf_ptr = torch.zeros(I, dtype=torch.int64, device=dev)
-        # I + 1 lines: line I (the walk's padding row) stays all zero
-        self.lines = torch.empty((I + 1) * 32, dtype=torch.int32, device=dev)
-        self.lines[I * 32:].zero_()
-        self.row_len = torch.empty(max(1, I), dtype=torch.int32, device=dev)
-        self.ws = torch.empty(max(1, N.lib().lg_spread_tile_rows_ws_bytes(I)),
-                              dtype=torch.uint8, device=dev)
-        self.ovf = torch.zeros(64 * 4, dtype=torch.int32, device=dev)
-        self.n_units = 0
+        self.g_bound = torch.empty((S, I), dtype=torch.int64, device=dev)
+        self.g_ovf_ptr = torch.zeros((S, I), dtype=torch.int64, device=dev)
+        # I + 1 lines per tile: line I (the walk's padding row) stays all zero
+        self.g_lines = torch.empty((S, (I + 1) * 32), dtype=torch.int32, device=dev)
+        self.g_lines[:, I * 32:].zero_()
+        self.g_row_len = torch.empty((S, max(1, I)), dtype=torch.int32, device=dev)
+        ws = (N.lib().lg_spread_tile_rows_ws_bytes(I) if S == 1
+              else N.lib().lg_spread_group_rows_ws_bytes(I, S))
+        self.ws = torch.empty(max(1, ws), dtype=torch.uint8, device=dev)
+        self.g_ovf = torch.zeros(64 * 4, dtype=torch.int32, device=dev)
+        self.g_base = torch.zeros(S, dtype=torch.int64, device=dev)
+        self._grp = None  # (first item, [widths], [ovf bases], [overflow units]) built
         self.j0 = None
         self.width = 0
         self._seek_at = None
@@ -514,48 +534,98 @@ class TileWeights:
 
     def build(self, j0: int, stop: int | None = None) -> None:
         """Build the tile [j0, min(j0 + tile, stop)); tiles come in ascending order from 0
-        (or from the item given to seek())."""
-        A, I, L = self.A, self.A.n_items, N.lib()
-        strm = N.stream_handle(self.dev)
+        (or from the item given to seek()). Builds the group starting at j0 unless j0 is the
+        next tile of the group already built."""
+        I = self.A.n_items
+        stop = I if stop is None else min(int(stop), I)
+        g = self._grp
+        if (g is not None and self._seek_at is None and self.j0 is not None
+                and j0 == self.j0 + self.width and j0 < g[0] + sum(g[1])):
+            self._select((j0 - g[0]) // self.tile)
+            return
         if self._seek_at is not None and j0 == self._seek_at:
             pass  # cursors placed by seek()
         elif j0 == 0:
-            self.cur.copy_(A.by_user.rowptr[:-1])
+            self.cur.copy_(self.A.by_user.rowptr[:-1])
         elif self.j0 is None or j0 != self.j0 + self.width:
             raise ValueError("tiles must be built in ascending order")
         else:
             self.cur, self.end = self.end, self.cur
         self._seek_at = None
-        stop = I if stop is None else min(int(stop), I)
-        width = min(self.tile, stop - j0)
-        if width <= 0:
+        if stop - j0 <= 0:
             raise ValueError(f"empty tile at {j0} (stop {stop})")
-        N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
-                                        A.n_users, j0 + width, N.ptr(self.cur),
-                                        N.ptr(self.end), N.ptr(self.count), strm),
-                "lg_spread_tile_cursor")
-        N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
-                                       N.ptr(self.count), N.ptr(self.bound), strm),
-                "lg_spread_tile_bound")
-        hub = self.bound > self.vthr
-        units = _run_units(torch.where(hub, torch.clamp(self.bound, max=width), self.bound), hub)
-        cum = torch.cumsum(units, 0)
-        torch.sub(cum, units, out=self.ovf_ptr)
-        total = int(cum[-1]) if I else 0  # host sync: sizes the overflow runs
-        if total + 64 >= 1 << 29:
+        widths = [min(self.tile, stop - t0) for t0 in
+                  range(j0, min(stop, j0 + self.group * self.tile), self.tile)]
+        self._build_group(j0, stop, widths)
+        self._select(0)
+
+    def _build_group(self, j0: int, stop: int, widths: list) -> None:
+        A, I, L = self.A, self.A.n_items, N.lib()
+        strm = N.stream_handle(self.dev)
+        nt = len(widths)
+        if self.group == 1:
+            N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
+                                            A.n_users, j0 + widths[0], N.ptr(self.cur),
+                                            N.ptr(self.end), N.ptr(self.counts), strm),
+                    "lg_spread_tile_cursor")
+            N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
+                                           N.ptr(self.counts), N.ptr(self.g_bound), strm),
+                    "lg_spread_tile_bound")
+        else:
+            N.check(L.lg_spread_group_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
+                                             A.n_users, j0, self.tile, nt, stop, N.ptr(self.cur),
+                                             N.ptr(self.end), N.ptr(self.counts), strm),
+                    "lg_spread_group_cursor")
+            N.check(L.lg_spread_group_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
+                                            N.ptr(self.counts), nt, N.ptr(self.g_bound), strm),
+                    "lg_spread_group_bound")
+        b = self.g_bound[:nt]
+        hub = b > self.vthr
+        wid = torch.tensor(widths, dtype=torch.int64, device=self.dev).view(nt, 1)
+        units = _run_units(torch.where(hub, torch.minimum(b, wid), b), hub)
+        cum = torch.cumsum(units, 1)
+        torch.sub(cum, units, out=self.g_ovf_ptr[:nt])
+        totals = cum[:, -1].tolist() if I else [0] * nt  # host sync: sizes the overflow runs
+        if max(totals) + 64 >= 1 << 29:
             raise ValueError("tile too large for the 29-bit overflow pointers (use a smaller tile)")
-        if (total + 64) * 4 > self.ovf.numel():
-            n = max((total + 64) * 4, int(self.ovf.numel() * 1.25))
-            self.ovf = torch.zeros(n, dtype=torch.int32, device=self.dev)
-        self.n_units = total
-        N.check(L.lg_spread_tile_rows_f64(
-            N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
-            N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count),
-            j0, self.tile, N.ptr(self.bound), self.vthr, N.ptr(self.ovf_ptr), N.ptr(self.lines),
-            N.ptr(self.ovf), N.ptr(self.row_len), N.ptr(self.ws), self.ws.numel(), strm),
-            "lg_spread_tile_rows_f64")
-        self.j0, self.width = j0, width
+        bases = [sum(totals[:t]) for t in range(nt)]
+        need = (sum(totals) + 64) * 4
+        if need > self.g_ovf.numel():
+            self.g_ovf = torch.zeros(max(need, int(self.g_ovf.numel() * 1.25)),
+                                     dtype=torch.int32, device=self.dev)
+        if self.group == 1:
+            N.check(L.lg_spread_tile_rows_f64(
+                N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
+                N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
+                N.ptr(self.counts), j0, self.tile, N.ptr(self.g_bound), self.vthr,
+                N.ptr(self.g_ovf_ptr), N.ptr(self.g_lines), N.ptr(self.g_ovf),
+                N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
+                "lg_spread_tile_rows_f64")
+        else:
+            self.g_base[:nt].copy_(torch.tensor(bases, dtype=torch.int64))
+            N.check(L.lg_spread_group_rows_f64(
+                N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
+                N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
+                N.ptr(self.counts), j0, self.tile, nt, N.ptr(self.g_bound), self.vthr,
+                N.ptr(self.g_ovf_ptr), N.ptr(self.g_base), N.ptr(self.g_lines),
+                N.ptr(self.g_ovf), N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(),
+                strm), "lg_spread_group_rows_f64")
+        self._grp = (j0, widths, bases, totals)
+
+    def _select(self, t: int) -> None:
+        """Make tile t of the built group the current tile (lines / ovf / bound / row_len
+        views, j0, width, n_units)."""
+        g0, widths, bases, totals = self._grp
+        I = self.A.n_items
+        self.j0, self.width = g0 + t * self.tile, widths[t]
+        self.lines = self.g_lines[t]
+        self.ovf = self.g_ovf[bases[t] * 4:]
+        self.bound = self.g_bound[t]
+        self.ovf_ptr = self.g_ovf_ptr[t]
+        self.row_len = self.g_row_len[t]
+        self.n_units = totals[t]
         if self.row_uses is not None:
+            hub = self.is_hub
             ln = self.row_len[:I].to(torch.int64)
             self.paths_read += (self.row_uses * ln).sum()
             used = _run_units(ln, hub)
@@ -596,7 +666,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
                       tile: int = 2048, scratch_bytes: int = 4 << 30,
                       items: slice | None = None, fused: bool | None = None,
-                      stats: dict | None = None):
+                      stats: dict | None = None, count_paths: bool = False):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). The values of spread_topk(A,
     hybrid_weight(spread_general(A), A.k_item, lam), ...) within a few ulp (the walk's
@@ -612,11 +682,13 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     merge_topk_lists, into the full lists: the multi-GPU item shard). fused=False keeps the
     two-kernel form (F columns of a span of tiles written to a [users, span] scratch of
     ``scratch_bytes``, then lg_tile_topk_f64; the same F values, so the same lists).
-    ``stats`` (optional dict) receives "w_paths": the paths the walk adds (sum over tiles and
-    users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the tile),
-    "w_bytes": the row bytes it gathers (one 128-byte line per (user, item) and tile, plus
-    16 bytes per overflow unit) and, on the fused path, the HIP-event times of the tile
-    builds / score bounds / walk launches (t_*_ms, walk_launches)."""
+    ``stats`` (optional dict) receives, on the fused path, the HIP-event times of the tile
+    builds / score bounds / walk launches (t_*_ms, walk_launches) and the walk's (user, item)
+    rows per launch; with ``count_paths`` also "w_paths": the paths the walk adds (sum over
+    tiles and users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the
+    tile) and "w_bytes": the row bytes it gathers (one 128-byte line per (user, item) and
+    tile, plus 16 bytes per overflow unit) -- extra GPU work per tile, so timed runs leave it
+    off and take the counts from tile_traffic()."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
@@ -634,12 +706,8 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     eu_r = None if eu is None else eu[u0:u1]
     if fused is None:
         fused = True
-    if stats is not None:
-        # users of each item among [u0, u1): the times its row is gathered per tile
-        cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
-        tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
-        tw.paths_read = torch.zeros((), dtype=torch.int64, device=dev)
-        tw.bytes_read = torch.zeros((), dtype=torch.int64, device=dev)
+    if stats is not None and count_paths:
+        _count_rows(tw, A, u0, u1)
     if fused:
         walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile)
         evs = [] if stats is not None else None
@@ -665,7 +733,8 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
             stats["t_bounds_ms"] = stats.get("t_bounds_ms", 0.0) + sum(e[1].elapsed_time(e[2]) for e in evs)
             stats["t_walk_ms"] = stats.get("t_walk_ms", 0.0) + sum(e[2].elapsed_time(e[3]) for e in evs)
             stats["walk_launches"] = stats.get("walk_launches", 0) + len(evs)
-            stats["user_items"] = stats.get("user_items", 0) + int(tw.row_uses.sum()) * len(evs)
+            stats["user_items"] = stats.get("user_items", 0) + len(evs) * int(
+                A.by_user.rowptr[u1] - A.by_user.rowptr[u0])
             stats["users"] = n
             stats["qstride"] = 0 if walk.d == 0 or walk.qbuf is None else walk.qbuf.shape[1]
             stats["nch"] = -(-tile // 64) if walk.d else 0
@@ -679,10 +748,37 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                 tw.build(j0, stop=i1)
                 tw.resource(u0, u1, F[:, j0 - s0:])
             tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
-    if stats is not None:
+    if stats is not None and count_paths:
         stats["w_paths"] = stats.get("w_paths", 0) + int(tw.paths_read)
         stats["w_bytes"] = stats.get("w_bytes", 0) + int(tw.bytes_read)
     return vals, idxs
+
+
+def _count_rows(tw: "TileWeights", A: Interactions, u0: int, u1: int) -> None:
+    """Make tw accumulate the walk's paths / row bytes for users [u0, u1) as tiles are
+    selected (the times each item's row is gathered per tile = its users in the range)."""
+    cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
+    tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
+    tw.paths_read = torch.zeros((), dtype=torch.int64, device=A.k_item.device)
+    tw.bytes_read = torch.zeros((), dtype=torch.int64, device=A.k_item.device)
+
+
+def tile_traffic(A: Interactions, tile: int = 2048, users: slice | None = None,
+                 items: slice | None = None) -> tuple[int, int]:
+    """(paths, row bytes) the tile walk of users / items gathers (the stats of
+    spread_topk_tiled(count_paths=True)), from the tiles alone: builds every tile, no walk."""
+    u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
+    i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
+                                                   min(A.n_items, items.stop))
+    if i1 <= i0 or u1 <= u0:
+        return 0, 0
+    tw = TileWeights(A, 0.5, min(int(tile), i1 - i0))
+    if i0:
+        tw.seek(i0)
+    _count_rows(tw, A, u0, u1)
+    for j0 in range(i0, i1, tw.tile):
+        tw.build(j0, stop=i1)
+    return int(tw.paths_read), int(tw.bytes_read)
 
 
 def row_norms(x: torch.Tensor) -> torch.Tensor:

@@ -20,6 +20,7 @@ ap.add_argument("--workload", default="c5-d64")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--unfused", action="store_true")
 ap.add_argument("--no-g", action="store_true", help="no G factor (SpreadMethod)")
+ap.add_argument("--count", action="store_true", help="count paths / row bytes (extra work)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
@@ -36,8 +37,10 @@ for rep in range(a.reps):
     st = {}
     ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile, fused=not a.unfused,
                           items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30,
-                          stats=st if rep == 0 else None, **kw)
+                          stats=st if rep == 0 else None, count_paths=a.count, **kw)
     torch.cuda.synchronize()
     dt = time.time() - t
     print(f"rep {rep}: {a.tiles} tiles x {U} users: {dt:.3f} s"
-          + (f"  paths {st['w_paths']:.3e} bytes {st['w_bytes']:.3e}" if st else ""), flush=True)
+          + (f"  paths {st.get('w_paths', 0):.3e} bytes {st.get('w_bytes', 0):.3e}"
+             f"  build {st.get('t_build_ms', 0):.1f} ms bounds {st.get('t_bounds_ms', 0):.1f} ms"
+             f" walk {st.get('t_walk_ms', 0):.1f} ms" if st else ""), flush=True)

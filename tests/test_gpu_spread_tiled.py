@@ -71,6 +71,37 @@ def test_tile_weights_and_resource(zipf, lam):
         assert hub_seen, "the zipf graph should exercise the hub-row path"
 
 
+@pytest.mark.parametrize("zipf,tile,group,vthr", [(False, 64, 8, None), (True, 100, 3, None),
+                                                  (True, 256, 8, None), (True, 128, 5, 40),
+                                                  (False, 1000, 8, None)])
+def test_group_build_equals_per_tile(zipf, tile, group, vthr):
+    """The group build (lg_spread_group_*: each (item, user) pair visited once per group of
+    tiles) writes every tile's lines, overflow runs, bounds and row lengths bit for bit as the
+    per-tile passes do, including hub (V) rows, overflow runs, a partial last group and a
+    stop inside a tile."""
+    from lgcnhs import ops
+    U, I = 700, 900
+    A = _inter(U, I, 30000 if zipf else 12000, seed=5, zipf=zipf)
+    stop = I - 37
+    a = ops.TileWeights(A, 0.5, tile, vthr=vthr, group=1)
+    b = ops.TileWeights(A, 0.5, tile, vthr=vthr, group=group)
+    hub_seen = ovf_seen = False
+    for j0 in range(0, stop, tile):
+        a.build(j0, stop)
+        b.build(j0, stop)
+        assert (a.j0, a.width, a.n_units) == (b.j0, b.width, b.n_units)
+        assert torch.equal(a.lines, b.lines)
+        assert torch.equal(a.bound, b.bound) and torch.equal(a.row_len, b.row_len)
+        # the runs themselves (a hub row's run may end before its allocated units, whose
+        # words are never read: compared through the decoder, which walks the headers)
+        assert np.array_equal(a.dense().view(np.uint64), b.dense().view(np.uint64))
+        hub_seen |= bool(a.is_hub.any())
+        ovf_seen |= a.n_units > 0
+    assert ovf_seen
+    if zipf:
+        assert hub_seen
+
+
 @pytest.mark.parametrize("k", [1, 10, 33, 100])
 @pytest.mark.parametrize("tile", [64, 333, 4096])
 @pytest.mark.parametrize("mode", ["G_drop", "drop", "none"])
@@ -279,7 +310,7 @@ def test_spread_stats_count_path_updates(fused):
     for users, items in ((slice(0, U), slice(0, I)), (slice(20, 90), slice(77, 301))):
         st = {}
         ops.spread_topk_tiled(A, 0.5, 10, A.by_user, tile=tile, users=users, items=items,
-                              fused=fused, stats=st)
+                              fused=fused, stats=st, count_paths=True)
         uses = Ad[users].sum(0)
         paths = nbytes = 0
         for j0 in range(items.start, items.stop, tile):
@@ -293,6 +324,8 @@ def test_spread_stats_count_path_updates(fused):
             nbytes += int((uses * (128 + 16 * units)).sum())
         assert st["w_paths"] == paths
         assert st["w_bytes"] == nbytes
+        # the untimed accounting the bench uses: the same counts from the tiles alone
+        assert ops.tile_traffic(A, tile, users=users, items=items) == (paths, nbytes)
     assert (C.sum(1) > tile).any(), "the zipf graph should have hub rows"
 
 
