@@ -284,12 +284,17 @@ int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_user
  *   (cur[v] = the first position with item >= group_begin; cur and end must not alias).
  * lg_spread_group_bound: bound[t][i] ([n_tiles][n_items] int64) = lg_spread_tile_bound of
  *   tile t.
+ * lg_spread_group_units: units[t][i] ([n_tiles][n_items] int64) = the overflow units of
+ *   row i in tile t (1 + ceil((bound - 31) / 4) for P rows with bound > 31, 1 + (min(bound,
+ *   width_t) - 7) for V rows with more than 7 entries, else 0); the caller's inclusive scan
+ *   of the flat array (units_incl) places every run: tile t's runs start at unit
+ *   units_incl[t n_items - 1] (0 for t = 0), each row's run at its exclusive prefix.
  * lg_spread_group_rows_f64: lg_spread_tile_rows_f64 of every tile t of the group, tile t's
  *   lines at lines + t (n_items + 1) 128 bytes (each tile's line n_items zeroed by the
- *   caller), its overflow runs at ovf + 16 ovf_base[t] bytes (ovf_base: device int64
- *   [n_tiles], in 16-byte units), ovf_ptr / row_len as [n_tiles][n_items] with the per-tile
- *   meaning of lg_spread_tile_rows_f64 (the same words bit for bit); vthr in [31, 65535];
- *   ws: lg_spread_group_rows_ws_bytes(n_items, n_tiles) bytes. */
+ *   caller), its runs in ovf as units_incl places them (header pointers relative to the
+ *   tile's first unit: each tile's lines and runs are the per-tile build's, bit for bit);
+ *   ovf holds units_incl[n_tiles n_items - 1] + 64 units; row_len as [n_tiles][n_items];
+ *   vthr in [31, 65535]; ws: lg_spread_group_rows_ws_bytes(n_items, n_tiles) bytes. */
 int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                            int64_t n_users, int32_t group_begin, int32_t tile, int32_t n_tiles,
                            int32_t stop, const int64_t *cur, int64_t *end, uint16_t *counts,
@@ -297,15 +302,17 @@ int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items
 int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *item_users,
                           int64_t n_items, const uint16_t *counts, int32_t n_tiles,
                           int64_t *bound, lg_stream_t stream);
+int lg_spread_group_units(const int64_t *bound, int64_t n_items, int32_t group_begin,
+                          int32_t tile, int32_t n_tiles, int32_t stop, int64_t vthr,
+                          int64_t *units, lg_stream_t stream);
 size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles);
 int lg_spread_group_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
                              const int32_t *user_items, const uint16_t *user_cls,
                              const double *inv_deg, int64_t n_items, const int64_t *cur,
                              const uint16_t *counts, int32_t group_begin, int32_t tile,
-                             int32_t n_tiles, const int64_t *bound, int64_t vthr,
-                             const int64_t *ovf_ptr, const int64_t *ovf_base, void *lines,
-                             void *ovf, int32_t *row_len, void *ws, size_t ws_bytes,
-                             lg_stream_t stream);
+                             int32_t n_tiles, int32_t stop, const int64_t *bound, int64_t vthr,
+                             const int64_t *units_incl, void *lines, void *ovf,
+                             int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream);
 
 /* F[u][j - item_begin] = rb[j] * sum over the paths of u's items of the tile's rows (see the
  * section comment) for the n_users rows of user_rowptr (pass user_rowptr + u0 for a block)

@@ -32,6 +32,7 @@
 // ascending-i order), then one multiply by rb_j. Against the reference's
 // general_W / (alpha (x) beta) summed by BLAS this is a few ulp per term (tests: 1e-12
 // relative), the reference's own BLAS order being unspecified.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "common.h"
@@ -374,6 +375,36 @@ __global__ __launch_bounds__(256) void k_group_bound(const int64_t *__restrict__
   }
 }
 
+// Overflow units (run header + data) of a row with nb pairs in a tile of width w: P rows
+// (nb <= vthr) 1 + ceil((nb - 31) / 4) past the line's 31 slots, V rows (hub items)
+// 1 + (min(nb, w) - 7) past the line's 7 entries, else 0 (= ops._run_units).
+__device__ __forceinline__ int64_t run_units(int64_t nb, int64_t vthr, int64_t w) {
+  if (nb > vthr) {
+    const int64_t len = nb < w ? nb : w;
+    return len > kLineEnts ? 1 + (len - kLineEnts) : 0;
+  }
+  return nb > kLineSlots ? 1 + (nb - kLineSlots + 3) / 4 : 0;
+}
+
+__device__ __forceinline__ int64_t tile_width(int32_t group_begin, int32_t tile, int t,
+                                              int32_t stop) {
+  const int64_t b = (int64_t)group_begin + (int64_t)t * tile;
+  const int64_t e = b + tile < stop ? b + tile : stop;
+  return e - b;
+}
+
+// units[t][i] = run_units of row i in tile t (the caller's inclusive scan over the flat
+// [n_tiles][n_items] array places the runs: tile by tile, rows ascending)
+__global__ __launch_bounds__(256) void k_group_units(const int64_t *__restrict__ bound,
+                                                     int64_t n_items, int32_t group_begin,
+                                                     int32_t tile, int32_t n_tiles, int32_t stop,
+                                                     int64_t vthr, int64_t *__restrict__ units) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n_items * n_tiles) return;
+  const int t = (int)(x / n_items);
+  units[x] = run_units(bound[x], vthr, tile_width(group_begin, tile, t, stop));
+}
+
 // P rows of every tile of the group: one wave per item row (tiles whose row is a hub row,
 // bound > vthr, are left to k_group_rows_hub). The lanes' counts of two tiles are scanned
 // together as 16-bit fields of one word: a P row's prefix never exceeds its bound <= vthr <
@@ -382,15 +413,21 @@ __global__ __launch_bounds__(256) void k_group_rows(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, const uint16_t *__restrict__ user_cls,
     int64_t n_items, const int64_t *__restrict__ cur, const uint4 *__restrict__ counts,
-    int32_t group_begin, int32_t tile, int32_t n_tiles, const int64_t *__restrict__ bound,
-    int64_t vthr, const int64_t *__restrict__ ovf_ptr, const int64_t *__restrict__ ovf_base,
+    int32_t group_begin, int32_t tile, int32_t n_tiles, int32_t stop,
+    const int64_t *__restrict__ bound, int64_t vthr, const int64_t *__restrict__ units_incl,
     uint32_t *__restrict__ lines, uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
   const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   if (i >= n_items) return;
   const int lane = lane_id();
-  const int64_t nbl = lane < n_tiles ? bound[(int64_t)lane * n_items + i] : 0;
-  const int64_t oul = lane < n_tiles ? ovf_ptr[(int64_t)lane * n_items + i] : 0;
-  const int64_t obl = lane < n_tiles ? ovf_base[lane] : 0;
+  // lane t < n_tiles: row i's pairs, run offset (relative to the tile's runs) and the
+  // tile's first unit in ovf
+  int64_t nbl = 0, oul = 0, obl = 0;
+  if (lane < n_tiles) {
+    const int64_t x = (int64_t)lane * n_items + i;
+    nbl = bound[x];
+    obl = lane ? units_incl[(int64_t)lane * n_items - 1] : 0;
+    oul = units_incl[x] - run_units(nbl, vthr, tile_width(group_begin, tile, lane, stop)) - obl;
+  }
   const int64_t tstride = (n_items + 1) * 32;  // words per tile of lines
   // P tiles of this row (wave-uniform)
   const uint32_t pmask = (uint32_t)__ballot(lane < n_tiles && nbl <= vthr);
@@ -492,8 +529,8 @@ __global__ __launch_bounds__(256) void k_group_rows_hub(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, const double *__restrict__ inv_deg,
     int64_t n_items, const int64_t *__restrict__ cur, const uint4 *__restrict__ counts,
-    int32_t group_begin, int32_t tile, const int64_t *__restrict__ ovf_ptr,
-    const int64_t *__restrict__ ovf_base, uint32_t *__restrict__ lines,
+    int32_t group_begin, int32_t tile, int32_t stop, const int64_t *__restrict__ bound,
+    int64_t vthr, const int64_t *__restrict__ units_incl, uint32_t *__restrict__ lines,
     uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
   extern __shared__ double acc[];  // tile doubles
   __shared__ int wsum[4];
@@ -517,8 +554,10 @@ __global__ __launch_bounds__(256) void k_group_rows_hub(
       __syncthreads();  // the next user may hit the same columns from other threads
     }
     uint32_t *line = lines + (int64_t)t * (n_items + 1) * 32 + i * 32;
-    uint32_t *ov = ovf + ovf_base[t] * 4;
-    const int64_t ou = ovf_ptr[flat];
+    const int64_t tbase = t ? units_incl[(int64_t)t * n_items - 1] : 0;
+    uint32_t *ov = ovf + tbase * 4;
+    const int64_t ou = units_incl[flat] -
+                       run_units(bound[flat], vthr, tile_width(group_begin, tile, t, stop)) - tbase;
     int base = 0;
     for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
       const int j = j0 + threadIdx.x;
@@ -923,6 +962,24 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
 //            only those columns get rb_j and (with G) the exact chain score. Ids grow along
 //            the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
 constexpr int MODE_F = 0, MODE_TOPK = 1;
+#ifndef LG_WALK_COUNT
+#define LG_WALK_COUNT 0  // measurement build: event counters of the top-K scan
+#endif
+#if LG_WALK_COUNT
+// [0] 512-column scan steps with a pre-screen pass, [1] pre-screen passes, [2] lanes x
+// drain rounds (/64 = rounds), [3] exact-score candidates, [4] lanes x rounds with an exact
+// score (/64), [5] insertions (/64); counted per lane with wave-level atomics
+__device__ unsigned long long g_walk_cnt[8];
+__device__ __forceinline__ void walk_count(int k, unsigned long long v) {
+  if (v) atomicAdd(&g_walk_cnt[k], v);
+}
+__device__ __forceinline__ void walk_count_lanes(int k, int v) {
+  uint64_t s = (uint64_t)v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane_id() == 0 && s) atomicAdd(&g_walk_cnt[k], (unsigned long long)s);
+}
+#endif
 constexpr int kWalkQ = 8;       // line loads per lane per batch: 8 rows each, 64 rows
 constexpr int kBatchRows = 8 * kWalkQ;
 constexpr int kOvfList = kBatchRows;
@@ -930,6 +987,9 @@ constexpr int kOvfList = kBatchRows;
 #define LG_DECODE_PHASE 4
 #endif
 constexpr int kDecodePhase = LG_DECODE_PHASE;
+// q dwords per lane loaded with the user's first batch (256 columns each), then streamed
+// kQPre / 2 scan iterations ahead (4 and 8 measured no faster than 2: 3.22 / 3.33 vs 3.20 s)
+constexpr int kQPre = 2;
   // lines whose class reads precede their adds
 static_assert(kWalkQ % kDecodePhase == 0, "decode phase must divide the batch's line loads");
 
@@ -1103,6 +1163,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   // lines and ra of a batch (rows past r1 read the zero line)
   auto load_rows = [&](const Batch &x, const int32_t (&it)[Q], uint4 (&w)[Q], double (&ra)[Q])
       __attribute__((always_inline)) {
+    // (every load group is issued even past a short last batch: skipping them with a
+    // uniform branch measured 40 % slower -- the branches cost the loads their overlap)
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int64_t r = x.r0 + 8 * q + grow;
@@ -1117,7 +1179,11 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   int lid0 = -1, lid1 = -1;
   double lv0 = 0.0, lv1 = 0.0;
   float gbv = 0.f;
-  uint32_t qd0 = 0xFFFFFFFFu;  // the per-column bounds of columns 4 lane .. + 3 (D > 0)
+  // the per-column bounds of the user's first kQPre * 256 columns (dword k: columns
+  // 256 k + 4 lane .. + 3), loaded with the user's first batch so the scan never waits
+  uint32_t qr[kQPre];
+#pragma unroll
+  for (int k = 0; k < kQPre; ++k) qr[k] = 0xFFFFFFFFu;
   int64_t xpos = 0, xhi = 0;
   int32_t xw = 0x7fffffff;
   auto load_user = [&](int64_t u) __attribute__((always_inline)) {
@@ -1140,7 +1206,12 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       }
       if constexpr (D > 0) {
         gbv = a.gb[u * a.nch + (lane < a.nch ? lane : 0)];
-        if (a.qb) qd0 = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + 4 * lane);
+        if (a.qb) {
+#pragma unroll
+          for (int k = 0; k < kQPre; ++k)
+            if (256 * k < a.qstride)
+              qr[k] = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + 256 * k + 4 * lane);
+        }
       }
       if (a.ex_rowptr) {
         xpos = a.ex_cur[u];
@@ -1376,14 +1447,14 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             q = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + c0 + 4 * lane);
         return q;
       };
-      uint32_t qn0 = qd0, qn1 = q_at(256);
       const double2 zero2{0.0, 0.0};
       for (int c0 = 0; c0 < a.width; c0 += 512) {
-        const uint32_t qa = qn0, qb2 = qn1;
-        if (c0 + 512 < a.width) {  // the next iteration's bounds, in flight during this one
-          qn0 = q_at(c0 + 512);
-          qn1 = q_at(c0 + 768);
-        }
+        const uint32_t qa = qr[0], qb2 = qr[1];
+#pragma unroll
+        for (int k = 0; k + 2 < kQPre; ++k) qr[k] = qr[k + 2];
+        // wider tiles: the bounds kQPre / 2 iterations ahead
+        qr[kQPre - 2] = q_at(c0 + 256 * kQPre);
+        qr[kQPre - 1] = q_at(c0 + 256 * kQPre + 256);
         double sv[8];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
@@ -1416,6 +1487,13 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           }
           mask |= pre ? 1u << t : 0u;
         }
+#if LG_WALK_COUNT
+        {
+          const bool any = __ballot(mask != 0) != 0;
+          if (lane == 0) walk_count(0, any ? 1 : 0);
+        }
+        walk_count_lanes(1, __popc(mask));
+#endif
         while (__ballot(mask != 0)) {
           const bool has = mask != 0;
           const int t = has ? __ffs(mask) - 1 : 0;
@@ -1430,7 +1508,14 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
                               __shfl(bq_v, (j >> 6) & 63);
             const bool cand = has && bq * f > tau;
+#if LG_WALK_COUNT
+            walk_count_lanes(2, 1);
+            walk_count_lanes(3, cand ? 1 : 0);
+#endif
             if (__ballot(cand)) {
+#if LG_WALK_COUNT
+              walk_count_lanes(4, 1);
+#endif
               need_us();
               double v = 0.0;
               const int item = a.item_begin + j;
@@ -1443,6 +1528,9 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
                 const int l = __ffsll((long long)bal) - 1;
                 bal &= bal - 1;
                 insert1(__shfl(v, l), __shfl(item, l));
+#if LG_WALK_COUNT
+                walk_count_lanes(5, 1);
+#endif
               }
             }
           } else {
@@ -1769,6 +1857,21 @@ extern "C" int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *
   return launch_status("lg_spread_group_bound");
 }
 
+extern "C" int lg_spread_group_units(const int64_t *bound, int64_t n_items, int32_t group_begin,
+                                     int32_t tile, int32_t n_tiles, int32_t stop, int64_t vthr,
+                                     int64_t *units, lg_stream_t stream) {
+  LG_REQUIRE(bound && units && n_items >= 0 && group_begin >= 0 && stop > group_begin &&
+                 vthr >= kLineSlots,
+             "lg_spread_group_units: bad arguments");
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
+             "lg_spread_group_units: tile %d / n_tiles %d", tile, n_tiles);
+  const int64_t n = n_items * n_tiles;
+  if (n == 0) return LG_OK;
+  k_group_units<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
+      bound, n_items, group_begin, tile, n_tiles, stop, vthr, units);
+  return launch_status("lg_spread_group_units");
+}
+
 extern "C" size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles) {
   return (size_t)(n_items * (n_tiles > 0 ? n_tiles : 1) + 1) * sizeof(int64_t);
 }
@@ -1776,11 +1879,11 @@ extern "C" size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles
 extern "C" int lg_spread_group_rows_f64(
     const int64_t *item_rowptr, const int32_t *item_users, const int32_t *user_items,
     const uint16_t *user_cls, const double *inv_deg, int64_t n_items, const int64_t *cur,
-    const uint16_t *counts, int32_t group_begin, int32_t tile, int32_t n_tiles,
-    const int64_t *bound, int64_t vthr, const int64_t *ovf_ptr, const int64_t *ovf_base,
-    void *lines, void *ovf, int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && counts && bound && ovf_ptr &&
-                 ovf_base && lines && ovf && n_items >= 0 && group_begin >= 0,
+    const uint16_t *counts, int32_t group_begin, int32_t tile, int32_t n_tiles, int32_t stop,
+    const int64_t *bound, int64_t vthr, const int64_t *units_incl, void *lines, void *ovf,
+    int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && counts && bound && units_incl &&
+                 lines && ovf && n_items >= 0 && group_begin >= 0 && stop > group_begin,
              "lg_spread_group_rows_f64: bad arguments");
   LG_REQUIRE(vthr >= kLineSlots && vthr < 65536,
              "lg_spread_group_rows_f64: vthr %lld not in [31, 65535]", (long long)vthr);
@@ -1803,13 +1906,14 @@ extern "C" int lg_spread_group_rows_f64(
   const uint4 *c4 = (const uint4 *)counts;
   k_group_rows<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, s>>>(
       item_rowptr, item_users, user_items, user_cls, n_items, cur, c4, group_begin, tile, n_tiles,
-      bound, vthr, ovf_ptr, ovf_base, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+      stop, bound, vthr, units_incl, (uint32_t *)lines, (uint32_t *)ovf, row_len);
   const int64_t nflat = n_items * n_tiles;
   k_hub_list<<<dim3((unsigned)((nflat + 255) / 256)), dim3(256), 0, s>>>(
       bound, nflat, vthr, (unsigned long long *)n_hub, hub_rows);
   k_group_rows_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
       hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, n_items, cur, c4,
-      group_begin, tile, ovf_ptr, ovf_base, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+      group_begin, tile, stop, bound, vthr, units_incl, (uint32_t *)lines, (uint32_t *)ovf,
+      row_len);
   return launch_status("lg_spread_group_rows_f64");
 }
 
@@ -1852,6 +1956,17 @@ static int launch_walk(const WalkArgs &a, hipStream_t s) {
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   const size_t lds = shared + (size_t)nw * per;
   k_tile_walk<MODE, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
+#if LG_WALK_COUNT
+  static int launches = 0;
+  if (++launches % 50 == 0 || a.item_begin + a.width >= a.null_row) {
+    unsigned long long h[8];
+    hipStreamSynchronize(s);
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_walk_cnt), sizeof(h));
+    fprintf(stderr, "[walk count] launches %d users %lld: steps_with_pass %llu passes %llu "
+            "rounds %llu cands %llu cand_rounds %llu inserts %llu\n", launches,
+            (long long)a.n_users, h[0], h[1], h[2] / 64, h[3], h[4] / 64, h[5] / 64);
+  }
+#endif
   return LG_OK;
 }
 

@@ -452,7 +452,12 @@ class TileWeights:
                 "lg_inv_degree_f64")
         self.user_cls, self.inv_cls = degree_classes(A.by_user.degrees())
         self.g_bound = torch.empty((S, I), dtype=torch.int64, device=dev)
-        self.g_ovf_ptr = torch.zeros((S, I), dtype=torch.int64, device=dev)
+        if S > 1:  # run units per (tile, row), their flat inclusive scan, the tiles' ends
+            self.g_units = torch.empty(S * I, dtype=torch.int64, device=dev)
+            self.g_incl = torch.empty(max(1, S * I), dtype=torch.int64, device=dev)
+            self._tile_ends = torch.arange(1, S + 1, dtype=torch.int64, device=dev) * I - 1
+            self._ends_host = torch.empty(S, dtype=torch.int64).pin_memory()
+            self._ends_ev = torch.cuda.Event()
         # I + 1 lines per tile: line I (the walk's padding row) stays all zero
         self.g_lines = torch.empty((S, (I + 1) * 32), dtype=torch.int32, device=dev)
         self.g_lines[:, I * 32:].zero_()
@@ -461,7 +466,6 @@ class TileWeights:
               else N.lib().lg_spread_group_rows_ws_bytes(I, S))
         self.ws = torch.empty(max(1, ws), dtype=torch.uint8, device=dev)
         self.g_ovf = torch.zeros(64 * 4, dtype=torch.int32, device=dev)
-        self.g_base = torch.zeros(S, dtype=torch.int64, device=dev)
         self._grp = None  # (first item, [widths], [ovf bases], [overflow units]) built
         self.j0 = None
         self.width = 0
@@ -563,7 +567,7 @@ class TileWeights:
         A, I, L = self.A, self.A.n_items, N.lib()
         strm = N.stream_handle(self.dev)
         nt = len(widths)
-        if self.group == 1:
+        if self.group == 1:  # the per-tile passes (their run placement by torch ops)
             N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
                                             A.n_users, j0 + widths[0], N.ptr(self.cur),
                                             N.ptr(self.end), N.ptr(self.counts), strm),
@@ -571,46 +575,66 @@ class TileWeights:
             N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
                                            N.ptr(self.counts), N.ptr(self.g_bound), strm),
                     "lg_spread_tile_bound")
-        else:
-            N.check(L.lg_spread_group_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
-                                             A.n_users, j0, self.tile, nt, stop, N.ptr(self.cur),
-                                             N.ptr(self.end), N.ptr(self.counts), strm),
-                    "lg_spread_group_cursor")
-            N.check(L.lg_spread_group_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
-                                            N.ptr(self.counts), nt, N.ptr(self.g_bound), strm),
-                    "lg_spread_group_bound")
-        b = self.g_bound[:nt]
-        hub = b > self.vthr
-        wid = torch.tensor(widths, dtype=torch.int64, device=self.dev).view(nt, 1)
-        units = _run_units(torch.where(hub, torch.minimum(b, wid), b), hub)
-        cum = torch.cumsum(units, 1)
-        torch.sub(cum, units, out=self.g_ovf_ptr[:nt])
-        totals = cum[:, -1].tolist() if I else [0] * nt  # host sync: sizes the overflow runs
-        if max(totals) + 64 >= 1 << 29:
-            raise ValueError("tile too large for the 29-bit overflow pointers (use a smaller tile)")
-        bases = [sum(totals[:t]) for t in range(nt)]
-        need = (sum(totals) + 64) * 4
-        if need > self.g_ovf.numel():
-            self.g_ovf = torch.zeros(max(need, int(self.g_ovf.numel() * 1.25)),
-                                     dtype=torch.int32, device=self.dev)
-        if self.group == 1:
+            b = self.g_bound[0]
+            hub = b > self.vthr
+            units = _run_units(torch.where(hub, torch.clamp(b, max=widths[0]), b), hub)
+            cum = torch.cumsum(units, 0)
+            ovf_ptr = cum - units
+            totals = [int(cum[-1]) if I else 0]  # host sync: sizes the overflow runs
+            bases = [0]
+            self._grow_ovf(totals[0])
             N.check(L.lg_spread_tile_rows_f64(
                 N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
                 N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
                 N.ptr(self.counts), j0, self.tile, N.ptr(self.g_bound), self.vthr,
-                N.ptr(self.g_ovf_ptr), N.ptr(self.g_lines), N.ptr(self.g_ovf),
+                N.ptr(ovf_ptr), N.ptr(self.g_lines), N.ptr(self.g_ovf),
                 N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
                 "lg_spread_tile_rows_f64")
+            self._grp = (j0, widths, bases, totals)
+            return
+        # group: cursors, bounds, run units and their inclusive scan all on the device; one
+        # event wait for the tiles' unit totals (to size ovf), then the rows
+        N.check(L.lg_spread_group_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
+                                         A.n_users, j0, self.tile, nt, stop, N.ptr(self.cur),
+                                         N.ptr(self.end), N.ptr(self.counts), strm),
+                "lg_spread_group_cursor")
+        N.check(L.lg_spread_group_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
+                                        N.ptr(self.counts), nt, N.ptr(self.g_bound), strm),
+                "lg_spread_group_bound")
+        if I:
+            units = self.g_units[:nt * I]
+            N.check(L.lg_spread_group_units(N.ptr(self.g_bound), I, j0, self.tile, nt, stop,
+                                            self.vthr, N.ptr(units), strm),
+                    "lg_spread_group_units")
+            incl = self.g_incl[:nt * I]
+            torch.cumsum(units, 0, out=incl)
+            ends = torch.index_select(incl, 0, self._tile_ends[:nt])
+            self._ends_host[:nt].copy_(ends, non_blocking=True)
+            self._ends_ev.record()
+            self._ends_ev.synchronize()  # the tiles' last units (not the whole stream's work)
+            ends = self._ends_host[:nt].tolist()
         else:
-            self.g_base[:nt].copy_(torch.tensor(bases, dtype=torch.int64))
-            N.check(L.lg_spread_group_rows_f64(
-                N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
-                N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
-                N.ptr(self.counts), j0, self.tile, nt, N.ptr(self.g_bound), self.vthr,
-                N.ptr(self.g_ovf_ptr), N.ptr(self.g_base), N.ptr(self.g_lines),
-                N.ptr(self.g_ovf), N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(),
-                strm), "lg_spread_group_rows_f64")
+            ends = [0] * nt
+        bases = [0] + ends[:-1]
+        totals = [e - b for e, b in zip(ends, bases)]
+        if ends[-1] + 64 >= 1 << 29:
+            raise ValueError("tile group too large for the 29-bit overflow pointers (use a "
+                             "smaller tile or group)")
+        self._grow_ovf(ends[-1])
+        N.check(L.lg_spread_group_rows_f64(
+            N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
+            N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
+            N.ptr(self.counts), j0, self.tile, nt, stop, N.ptr(self.g_bound), self.vthr,
+            N.ptr(self.g_incl), N.ptr(self.g_lines), N.ptr(self.g_ovf),
+            N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
+            "lg_spread_group_rows_f64")
         self._grp = (j0, widths, bases, totals)
+
+    def _grow_ovf(self, units: int) -> None:
+        need = (units + 64) * 4
+        if need > self.g_ovf.numel():
+            self.g_ovf = torch.zeros(max(need, int(self.g_ovf.numel() * 1.25)),
+                                     dtype=torch.int32, device=self.dev)
 
     def _select(self, t: int) -> None:
         """Make tile t of the built group the current tile (lines / ovf / bound / row_len
@@ -621,7 +645,6 @@ class TileWeights:
         self.lines = self.g_lines[t]
         self.ovf = self.g_ovf[bases[t] * 4:]
         self.bound = self.g_bound[t]
-        self.ovf_ptr = self.g_ovf_ptr[t]
         self.row_len = self.g_row_len[t]
         self.n_units = totals[t]
         if self.row_uses is not None:
