@@ -281,7 +281,9 @@ int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_user
  * is [group_begin + t tile, min(group_begin + (t + 1) tile, stop)).
  * lg_spread_group_cursor: counts[v][0..7] (8 uint16 per user, 16-byte aligned, unused
  *   tiles 0) = user v's items in each tile, end[v] = the position after the group's last
- *   (cur[v] = the first position with item >= group_begin; cur and end must not alias).
+ *   (cur[v] = the first position with item >= group_begin; cur and end must not alias;
+ *   positions < 2^32), rec[v] (16 bytes per user, 16-byte aligned) = the user's record for
+ *   the rows pass: its class (user_cls) and up to 6 of its group items in place, else cur.
  * lg_spread_group_bound: bound[t][i] ([n_tiles][n_items] int64) = lg_spread_tile_bound of
  *   tile t.
  * lg_spread_group_units: units[t][i] ([n_tiles][n_items] int64) = the overflow units of
@@ -294,11 +296,12 @@ int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_user
  *   caller), its runs in ovf as units_incl places them (header pointers relative to the
  *   tile's first unit: each tile's lines and runs are the per-tile build's, bit for bit);
  *   ovf holds units_incl[n_tiles n_items - 1] + 64 units; row_len as [n_tiles][n_items];
- *   vthr in [31, 65535]; ws: lg_spread_group_rows_ws_bytes(n_items, n_tiles) bytes. */
+ *   vthr in [31, 65535]; cur / counts / rec from lg_spread_group_cursor; ws:
+ *   lg_spread_group_rows_ws_bytes(n_items, n_tiles) bytes. */
 int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
-                           int64_t n_users, int32_t group_begin, int32_t tile, int32_t n_tiles,
-                           int32_t stop, const int64_t *cur, int64_t *end, uint16_t *counts,
-                           lg_stream_t stream);
+                           const uint16_t *user_cls, int64_t n_users, int32_t group_begin,
+                           int32_t tile, int32_t n_tiles, int32_t stop, const int64_t *cur,
+                           int64_t *end, uint16_t *counts, void *rec, lg_stream_t stream);
 int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *item_users,
                           int64_t n_items, const uint16_t *counts, int32_t n_tiles,
                           int64_t *bound, lg_stream_t stream);
@@ -307,9 +310,9 @@ int lg_spread_group_units(const int64_t *bound, int64_t n_items, int32_t group_b
                           int64_t *units, lg_stream_t stream);
 size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles);
 int lg_spread_group_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                             const int32_t *user_items, const uint16_t *user_cls,
-                             const double *inv_deg, int64_t n_items, const int64_t *cur,
-                             const uint16_t *counts, int32_t group_begin, int32_t tile,
+                             const int32_t *user_items, const double *inv_deg,
+                             int64_t n_items, const int64_t *cur, const uint16_t *counts,
+                             const void *rec, int32_t group_begin, int32_t tile,
                              int32_t n_tiles, int32_t stop, const int64_t *bound, int64_t vthr,
                              const int64_t *units_incl, void *lines, void *ovf,
                              int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream);

@@ -315,31 +315,56 @@ constexpr int kGroupMax = 8;
 // counts[v][t] (kGroupMax uint16 per user) = the items of user v in tile t of the group
 // ([group_begin + t tile, min(group_begin + (t + 1) tile, stop))), end[v] = the position
 // after the group's last; cur[v] = the first position with item >= group_begin.
+// rec[v] (16 bytes, what k_group_rows gathers per (item, user) pair instead of counts, cur,
+// the class and the items): x = n (the user's items in the group, saturated at 255) |
+// class << 8; for n <= kRecItems the items as 16-bit codes t << 13 | (item - tile t's
+// first item) in y, z, w (low half first); else y = cur[v] (the rows read user_items).
+constexpr int kRecItems = 6;
 __global__ __launch_bounds__(256) void k_group_cursor(const int64_t *__restrict__ user_rowptr,
                                                       const int32_t *__restrict__ user_items,
+                                                      const uint16_t *__restrict__ user_cls,
                                                       int64_t n_users, int32_t group_begin,
                                                       int32_t tile, int32_t n_tiles,
                                                       int32_t stop, const int64_t *__restrict__ cur,
                                                       int64_t *__restrict__ end,
-                                                      uint4 *__restrict__ counts) {
+                                                      uint4 *__restrict__ counts,
+                                                      uint4 *__restrict__ rec) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_users) return;
-  int64_t p = cur[v];
+  const int64_t p0 = cur[v];
+  int64_t p = p0;
   const int64_t pe = user_rowptr[v + 1];
   uint32_t c[kGroupMax];
+  uint32_t code[kRecItems];
+#pragma unroll
+  for (int k = 0; k < kRecItems; ++k) code[k] = 0;
+  int n = 0;
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) {
     c[t] = 0;
     if (t < n_tiles) {
-      const int64_t l = (int64_t)group_begin + (int64_t)(t + 1) * tile;
+      const int32_t tb = group_begin + t * tile;
+      const int64_t l = (int64_t)tb + tile;
       const int32_t lim = (int32_t)(l < stop ? l : stop);
-      const int64_t p0 = p;
-      while (p < pe && user_items[p] < lim) ++p;
-      c[t] = (uint32_t)(p - p0);  // <= tile <= 8192
+      const int64_t pt = p;
+      for (; p < pe; ++p) {
+        const int32_t it = user_items[p];
+        if (it >= lim) break;
+        const uint32_t cd = (uint32_t)t << 13 | (uint32_t)(it - tb);
+#pragma unroll
+        for (int k = 0; k < kRecItems; ++k)
+          if (n == k) code[k] = cd;
+        ++n;
+      }
+      c[t] = (uint32_t)(p - pt);  // <= tile <= 8192
     }
   }
   end[v] = p;
   counts[v] = uint4{c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16};
+  const uint32_t hx = (uint32_t)(n < 255 ? n : 255) | (uint32_t)user_cls[v] << 8;
+  rec[v] = n <= kRecItems
+               ? uint4{hx, code[0] | code[1] << 16, code[2] | code[3] << 16, code[4] | code[5] << 16}
+               : uint4{hx, (uint32_t)p0, 0u, 0u};
 }
 
 __device__ __forceinline__ uint32_t count_of(const uint4 &c, int t) {
@@ -411,10 +436,10 @@ __global__ __launch_bounds__(256) void k_group_units(const int64_t *__restrict__
 // 2^16, and hub tiles' counts are masked to 0 before the scan.
 __global__ __launch_bounds__(256) void k_group_rows(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
-    const int32_t *__restrict__ user_items, const uint16_t *__restrict__ user_cls,
-    int64_t n_items, const int64_t *__restrict__ cur, const uint4 *__restrict__ counts,
-    int32_t group_begin, int32_t tile, int32_t n_tiles, int32_t stop,
-    const int64_t *__restrict__ bound, int64_t vthr, const int64_t *__restrict__ units_incl,
+    const int32_t *__restrict__ user_items, int64_t n_items, const uint4 *__restrict__ counts,
+    const uint4 *__restrict__ rec, int32_t group_begin, int32_t tile, int32_t n_tiles,
+    int32_t stop, const int64_t *__restrict__ bound, int64_t vthr,
+    const int64_t *__restrict__ units_incl,
     uint32_t *__restrict__ lines, uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
   const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   if (i >= n_items) return;
@@ -450,11 +475,31 @@ __global__ __launch_bounds__(256) void k_group_rows(
   const int64_t e1 = item_rowptr[i + 1];
   for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
     const int64_t e = e0 + lane;
-    uint4 c4{0u, 0u, 0u, 0u};
+    uint4 rc{0u, 0u, 0u, 0u};
     int32_t v = 0;
     if (e < e1) {
       v = item_users[e];
+      rc = rec[v];
+    }
+    const uint32_t nu = rc.x & 0xFFu;  // the user's items in the group
+    const bool longu = nu > (uint32_t)kRecItems;
+    uint4 c4{0u, 0u, 0u, 0u};
+    if (longu) {
       c4 = counts[v];
+    } else {  // per-tile counts from the item codes (ascending: tiles in order)
+#pragma unroll
+      for (int k = 0; k < kRecItems; ++k) {
+        const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
+        const uint32_t cd = (k & 1) ? wd >> 16 : wd & 0xFFFFu;
+        if ((uint32_t)k < nu) {
+          const uint32_t t = cd >> 13;
+          const uint32_t inc = 1u << (16 * (t & 1));
+          c4.x += t >> 1 == 0 ? inc : 0u;
+          c4.y += t >> 1 == 1 ? inc : 0u;
+          c4.z += t >> 1 == 2 ? inc : 0u;
+          c4.w += t >> 1 == 3 ? inc : 0u;
+        }
+      }
     }
     // hub tiles' counts masked out (their items still advance the lane's offset)
     uint32_t m4[4];
@@ -466,12 +511,8 @@ __global__ __launch_bounds__(256) void k_group_rows(
     }
     const uint32_t w[4] = {c4.x & m4[0], c4.y & m4[1], c4.z & m4[2], c4.w & m4[3]};
     if (__ballot((w[0] | w[1] | w[2] | w[3]) != 0) == 0) continue;  // no pair in any P tile
-    int64_t s0 = 0;
-    uint32_t cl = 0;
-    if ((c4.x | c4.y | c4.z | c4.w) != 0) {
-      s0 = cur[v];
-      cl = (uint32_t)user_cls[v];
-    }
+    const int64_t s0 = longu ? (int64_t)rc.y : 0;
+    const uint32_t cl = rc.x >> 8;
     uint32_t off = 0;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
@@ -497,9 +538,17 @@ __global__ __launch_bounds__(256) void k_group_rows(
           uint32_t *ov = ovf + __shfl(obl, t) * 4;
           const int64_t ou = __shfl(oul, t);
           const int32_t ib = group_begin + t * tile;
-          for (uint32_t q = 0; q < ct; ++q)
-            put_slot(line, ov, ou, n[t] + pb + q,
-                     (cl << 16) | (uint32_t)(user_items[s0 + off + q] - ib));
+          for (uint32_t q = 0; q < ct; ++q) {
+            uint32_t jr;
+            if (longu) {
+              jr = (uint32_t)(user_items[s0 + off + q] - ib);
+            } else {
+              const uint32_t k = off + q;
+              const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
+              jr = ((k & 1) ? wd >> 16 : wd) & 0x1FFFu;
+            }
+            put_slot(line, ov, ou, n[t] + pb + q, (cl << 16) | jr);
+          }
           if (ct && cl >= (uint32_t)kInvTab) farbits |= 1u << t;
           n[t] += tot;
         }
@@ -1829,19 +1878,22 @@ extern "C" int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t
 }
 
 extern "C" int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
-                                      int64_t n_users, int32_t group_begin, int32_t tile,
-                                      int32_t n_tiles, int32_t stop, const int64_t *cur,
-                                      int64_t *end, uint16_t *counts, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && cur && end && counts && n_users >= 0 && cur != end &&
-                 group_begin >= 0 && stop > group_begin,
+                                      const uint16_t *user_cls, int64_t n_users,
+                                      int32_t group_begin, int32_t tile, int32_t n_tiles,
+                                      int32_t stop, const int64_t *cur, int64_t *end,
+                                      uint16_t *counts, void *rec, lg_stream_t stream) {
+  LG_REQUIRE(user_rowptr && user_cls && cur && end && counts && rec && n_users >= 0 &&
+                 cur != end && group_begin >= 0 && stop > group_begin,
              "lg_spread_group_cursor: bad arguments");
+  LG_REQUIRE(((uintptr_t)rec & 15) == 0, "lg_spread_group_cursor: rec not 16-byte aligned");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
              "lg_spread_group_cursor: tile %d / n_tiles %d", tile, n_tiles);
   LG_REQUIRE(((uintptr_t)counts & 15) == 0, "lg_spread_group_cursor: counts not 16-byte aligned");
   if (n_users == 0) return LG_OK;
   k_group_cursor<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0,
-                   (hipStream_t)stream>>>(user_rowptr, user_items, n_users, group_begin, tile,
-                                          n_tiles, stop, cur, end, (uint4 *)counts);
+                   (hipStream_t)stream>>>(user_rowptr, user_items, user_cls, n_users,
+                                          group_begin, tile, n_tiles, stop, cur, end,
+                                          (uint4 *)counts, (uint4 *)rec);
   return launch_status("lg_spread_group_cursor");
 }
 
@@ -1878,11 +1930,11 @@ extern "C" size_t lg_spread_group_rows_ws_bytes(int64_t n_items, int32_t n_tiles
 
 extern "C" int lg_spread_group_rows_f64(
     const int64_t *item_rowptr, const int32_t *item_users, const int32_t *user_items,
-    const uint16_t *user_cls, const double *inv_deg, int64_t n_items, const int64_t *cur,
-    const uint16_t *counts, int32_t group_begin, int32_t tile, int32_t n_tiles, int32_t stop,
+    const double *inv_deg, int64_t n_items, const int64_t *cur, const uint16_t *counts,
+    const void *rec, int32_t group_begin, int32_t tile, int32_t n_tiles, int32_t stop,
     const int64_t *bound, int64_t vthr, const int64_t *units_incl, void *lines, void *ovf,
     int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_cls && inv_deg && cur && counts && bound && units_incl &&
+  LG_REQUIRE(item_rowptr && rec && inv_deg && cur && counts && bound && units_incl &&
                  lines && ovf && n_items >= 0 && group_begin >= 0 && stop > group_begin,
              "lg_spread_group_rows_f64: bad arguments");
   LG_REQUIRE(vthr >= kLineSlots && vthr < 65536,
@@ -1905,8 +1957,8 @@ extern "C" int lg_spread_group_rows_f64(
   }
   const uint4 *c4 = (const uint4 *)counts;
   k_group_rows<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, s>>>(
-      item_rowptr, item_users, user_items, user_cls, n_items, cur, c4, group_begin, tile, n_tiles,
-      stop, bound, vthr, units_incl, (uint32_t *)lines, (uint32_t *)ovf, row_len);
+      item_rowptr, item_users, user_items, n_items, c4, (const uint4 *)rec, group_begin, tile,
+      n_tiles, stop, bound, vthr, units_incl, (uint32_t *)lines, (uint32_t *)ovf, row_len);
   const int64_t nflat = n_items * n_tiles;
   k_hub_list<<<dim3((unsigned)((nflat + 255) / 256)), dim3(256), 0, s>>>(
       bound, nflat, vthr, (unsigned long long *)n_hub, hub_rows);

@@ -81,14 +81,14 @@ SIGNATURES = {
         [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp,
          _vp, _sz, _vp],
     ),
-    "lg_spread_group_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp,
-                                              _vp, _vp]),
+    "lg_spread_group_cursor": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
+                                              _vp, _vp, _vp, _vp]),
     "lg_spread_group_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _vp, _vp]),
     "lg_spread_group_units": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i32, _i32, _i64, _vp, _vp]),
     "lg_spread_group_rows_ws_bytes": (_sz, [_i64, _i32]),
     "lg_spread_group_rows_f64": (
         ctypes.c_int,
-        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
+        [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
          _vp, _vp, _vp, _sz, _vp],
     ),
     "lg_spread_tile_resource_f64": (

@@ -444,8 +444,11 @@ class TileWeights:
         self.end = torch.empty_like(self.cur)
         if S == 1:
             self.counts = torch.empty(A.n_users, dtype=torch.uint16, device=dev)
-        else:  # 8 uint16 per user (one 16-byte load)
+        else:  # 8 uint16 per user (one 16-byte load) + the rows pass's 16-byte records
+            if int(A.by_user.rowptr[-1]) >= 1 << 32:
+                raise ValueError("more than 2^32 interactions: use group=1")
             self.counts = torch.empty((A.n_users, 8), dtype=torch.uint16, device=dev)
+            self.rec = torch.empty((A.n_users, 4), dtype=torch.int32, device=dev)
         self.inv_deg = torch.empty(A.n_users, dtype=torch.float64, device=dev)
         N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,
                                           N.ptr(self.inv_deg), N.stream_handle(dev)),
@@ -595,8 +598,9 @@ class TileWeights:
         # group: cursors, bounds, run units and their inclusive scan all on the device; one
         # event wait for the tiles' unit totals (to size ovf), then the rows
         N.check(L.lg_spread_group_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
-                                         A.n_users, j0, self.tile, nt, stop, N.ptr(self.cur),
-                                         N.ptr(self.end), N.ptr(self.counts), strm),
+                                         N.ptr(self.user_cls), A.n_users, j0, self.tile, nt,
+                                         stop, N.ptr(self.cur), N.ptr(self.end),
+                                         N.ptr(self.counts), N.ptr(self.rec), strm),
                 "lg_spread_group_cursor")
         N.check(L.lg_spread_group_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
                                         N.ptr(self.counts), nt, N.ptr(self.g_bound), strm),
@@ -623,8 +627,8 @@ class TileWeights:
         self._grow_ovf(ends[-1])
         N.check(L.lg_spread_group_rows_f64(
             N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
-            N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
-            N.ptr(self.counts), j0, self.tile, nt, stop, N.ptr(self.g_bound), self.vthr,
+            N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.counts), N.ptr(self.rec),
+            j0, self.tile, nt, stop, N.ptr(self.g_bound), self.vthr,
             N.ptr(self.g_incl), N.ptr(self.g_lines), N.ptr(self.g_ovf),
             N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
             "lg_spread_group_rows_f64")
