@@ -1090,6 +1090,20 @@ __device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
   __hip_atomic_fetch_add(&acc[col], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The fast decode's two LDS addresses of a P slot s (class << 16 | column, column < 8192),
+// one VALU op each: fl(1/k) of the class at byte s >> 13 (s_inv at LDS address 0; bits
+// 13-15 of the column are 0), and the column's acc entry at acc_base + 8 (s & 0xFFFF).
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ double slot_inv_fast(uint32_t s) {
+  return *(const lds_f64 *)(uintptr_t)(s >> 13);
+}
+__device__ __forceinline__ void slot_add_fast(uint32_t acc_base, uint32_t s, double v) {
+  uint32_t addr;
+  asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(addr) : "v"(s), "v"(acc_base));
+  __hip_atomic_fetch_add((lds_f64 *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // fl(1/k) of a P slot's degree class (general decode: classes >= kInvTab from memory)
 __device__ __forceinline__ double slot_inv(uint32_t s, const double *s_inv,
                                            const double *__restrict__ g_inv) {
@@ -1153,6 +1167,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   char *mine = reinterpret_cast<char *>(s_rb + tile) +
                (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
+  const uint32_t acc_base = (uint32_t)(uintptr_t)(lds_f64 *)acc;
   double *ovl_ra = acc + tile;  // overflow list (decode)
   uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
   float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);  // the user's row (D > 0)
@@ -1319,17 +1334,21 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         double inv[H][4];
 #pragma unroll
         for (int q = 0; q < H; ++q) {
-          inv[q][0] = s_inv[(w[q0 + q].x & hmask) >> 16];
-          inv[q][1] = s_inv[w[q0 + q].y >> 16];
-          inv[q][2] = s_inv[w[q0 + q].z >> 16];
-          inv[q][3] = s_inv[w[q0 + q].w >> 16];
+          inv[q][0] = slot_inv_fast(w[q0 + q].x & hmask);
+          inv[q][1] = slot_inv_fast(w[q0 + q].y);
+          inv[q][2] = slot_inv_fast(w[q0 + q].z);
+          inv[q][3] = slot_inv_fast(w[q0 + q].w);
         }
 #pragma unroll
         for (int q = 0; q < H; ++q) {
           const uint32_t sv[4] = {w[q0 + q].x & hmask, w[q0 + q].y, w[q0 + q].z, w[q0 + q].w};
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            if (sv[t]) lds_add(acc, sv[t] & 0xFFFFu, inv[q][t] * ra[q0 + q]);
+#if LG_DBG_SEQ_ADDS  // measurement build: the same adds at conflict-free addresses
+            if (sv[t]) lds_add(acc, (uint32_t)(lane * 4 + t), inv[q][t] * ra[q0 + q]);
+#else
+            if (sv[t]) slot_add_fast(acc_base, sv[t], inv[q][t] * ra[q0 + q]);
+#endif
         }
       }
     } else {

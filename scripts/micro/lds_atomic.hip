@@ -8,6 +8,8 @@
 
 constexpr int kCols = 2048;
 
+// MODE 0 / 4 / 5: ds_add_f64 with all lanes at random columns / ~45 % of the lanes active
+// (random mask, the walk's slot density) / all lanes at consecutive columns (conflict-free)
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_scatter(double *out, int iters, uint32_t seed) {
   extern __shared__ double lds[];
@@ -24,6 +26,12 @@ __global__ __launch_bounds__(1024) void k_scatter(double *out, int iters, uint32
       const uint32_t c = (x >> 8) & (kCols - 1);
       if constexpr (MODE == 0)
         __hip_atomic_fetch_add(&acc[c], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else if constexpr (MODE == 4) {
+        if (((x >> 3) & 15) < 7)  // 7 / 16 of the lanes
+          __hip_atomic_fetch_add(&acc[c], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if constexpr (MODE == 5)
+        __hip_atomic_fetch_add(&acc[(lane + 64 * s) & (kCols - 1)], v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
       else if constexpr (MODE == 1)
         __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(acc) + c, 3ull,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -74,6 +82,8 @@ int main() {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   run<0>("ds_add_f64", out, cus);
+  run<4>("add_f64 45%", out, cus);
+  run<5>("add_f64 seq", out, cus);
   run<1>("ds_add_u64", out, cus);
   run<2>("ds_add_f32", out, cus);
   run<3>("ds_write_b64", out, cus);
