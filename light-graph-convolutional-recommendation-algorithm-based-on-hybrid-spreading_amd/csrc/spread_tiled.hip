@@ -1011,6 +1011,9 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
 //            only those columns get rb_j and (with G) the exact chain score. Ids grow along
 //            the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
 constexpr int MODE_F = 0, MODE_TOPK = 1;
+#ifndef LG_BRANCHLESS
+#define LG_BRANCHLESS 1  // empty slots add 0.0 to a per-lane dummy (no branch per slot)
+#endif
 #ifndef LG_WALK_COUNT
 #define LG_WALK_COUNT 0  // measurement build: event counters of the top-K scan
 #endif
@@ -1103,6 +1106,16 @@ __device__ __forceinline__ void slot_add_fast(uint32_t acc_base, uint32_t s, dou
   __hip_atomic_fetch_add((lds_f64 *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// Branch-free form: an empty slot (s == 0, value 0) adds its 0.0 to the lane's own dummy
+// word instead (no exec-mask branch per slot; the dummies are lane-distinct: no conflicts).
+__device__ __forceinline__ void slot_add_nobranch(uint32_t acc_base, uint32_t dummy, uint32_t s,
+                                                  double v) {
+  uint32_t addr;
+  asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(addr) : "v"(s), "v"(acc_base));
+  addr = s ? addr : dummy;
+  __hip_atomic_fetch_add((lds_f64 *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // fl(1/k) of a P slot's degree class (general decode: classes >= kInvTab from memory)
 __device__ __forceinline__ double slot_inv(uint32_t s, const double *s_inv,
@@ -1168,6 +1181,9 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
                (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
   const uint32_t acc_base = (uint32_t)(uintptr_t)(lds_f64 *)acc;
+  // the lane's dummy word for empty slots: its entry of the overflow list (rewritten before
+  // every use; adding 0.0 leaves it unchanged meanwhile)
+  const uint32_t dummy_addr = acc_base + 8u * (uint32_t)(tile + lane);
   double *ovl_ra = acc + tile;  // overflow list (decode)
   uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
   float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);  // the user's row (D > 0)
@@ -1347,7 +1363,11 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #if LG_DBG_SEQ_ADDS  // measurement build: the same adds at conflict-free addresses
             if (sv[t]) lds_add(acc, (uint32_t)(lane * 4 + t), inv[q][t] * ra[q0 + q]);
 #else
+#if LG_BRANCHLESS
+            slot_add_nobranch(acc_base, dummy_addr, sv[t], inv[q][t] * ra[q0 + q]);
+#else
             if (sv[t]) slot_add_fast(acc_base, sv[t], inv[q][t] * ra[q0 + q]);
+#endif
 #endif
         }
       }
