@@ -29,6 +29,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBoundMargin = 0.008f;
+#ifndef LG_BOUND_DEPTH
+#define LG_BOUND_DEPTH 1  // item-fragment chunks in flight ahead (2 measured no faster at D = 64)
+#endif
 
 __device__ __forceinline__ float round_up_f32(double x) {
   float f = (float)x;
@@ -105,9 +108,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   bf16x8 fa[4][S], fb[4][S];
   float na = 0.f, nb = 0.f;
   load_items(0, fa, na);
+  // D <= 64: chunk c + 2's fragments in flight during chunk c (c + 1's already landed);
+  // D = 128 keeps one chunk ahead (the registers of a third set would spill)
+  constexpr bool kDeep = LG_BOUND_DEPTH > 1 && D <= 64;
+  bf16x8 fc[4][S];
+  float nc = 0.f;
+  if (kDeep && nch > 1) load_items(64, fb, nb);
   for (int c = 0; c < nch; ++c) {
     const int cb = 64 * c;  // chunk start inside the tile
-    if (c + 1 < nch) load_items(cb + 64, fb, nb);
+    if constexpr (kDeep) {
+      if (c + 2 < nch) load_items(cb + 128, fc, nc);
+    } else {
+      if (c + 1 < nch) load_items(cb + 64, fb, nb);
+    }
     // the chunk's largest item norm (wave-uniform)
     float inm = na;
 #pragma unroll
@@ -196,6 +209,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int s = 0; s < S; ++s) fa[t][s] = fb[t][s];
     na = nb;
+    if constexpr (kDeep) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < S; ++s) fb[t][s] = fc[t][s];
+      nb = nc;
+    }
   }
 }
 

@@ -1011,6 +1011,9 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
 //            only those columns get rb_j and (with G) the exact chain score. Ids grow along
 //            the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
 constexpr int MODE_F = 0, MODE_TOPK = 1;
+#ifndef LG_BUFFER_LOADS
+#define LG_BUFFER_LOADS 1  // batch loads through buffer descriptors (32-bit offsets)
+#endif
 #ifndef LG_BRANCHLESS
 #define LG_BRANCHLESS 1  // empty slots add 0.0 to a per-lane dummy (no branch per slot)
 #endif
@@ -1231,6 +1234,41 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     return new_user();
   };
   // item ids of a batch's rows (lanes of one 8-lane group: one row)
+#if LG_BUFFER_LOADS
+  // Buffer loads with 32-bit offsets: a batch's item ids and ra through a descriptor based
+  // at its first row (lane offsets are per-lane constants + immediates; rows past the batch
+  // are out of range and read 0), the lines through one descriptor for the tile.
+  const __amdgpu_buffer_rsrc_t r_lines = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.lines, 0, (int)((uint32_t)(a.null_row + 1) * 128u), 0x00020000);
+  auto load_ids = [&](const Batch &x, int32_t (&it)[Q]) __attribute__((always_inline)) {
+    if (x.r1 > x.r0) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(a.user_items + x.r0), 0, (int)((x.r1 - x.r0) * 4), 0x00020000);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        it[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(grow * 4 + 32 * q),
+                                                              0, 0);
+    }
+  };
+  // lines and ra of a batch (rows past r1 read the zero line, and ra 0)
+  auto load_rows = [&](const Batch &x, const int32_t (&it)[Q], uint4 (&w)[Q], double (&ra)[Q])
+      __attribute__((always_inline)) {
+    // (every load group is issued even past a short last batch: skipping them with a
+    // uniform branch measured 40 % slower -- the branches cost the loads their overlap)
+    const int nr = (int)(x.r1 - x.r0);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.ra_edge + x.r0), 0, nr * 8, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const bool in = 8 * q + grow < nr;
+      const uint32_t row = in ? (uint32_t)it[q] : (uint32_t)a.null_row;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r_lines, row * 128u + 16u * gh, 0, 0);
+      w[q] = uint4{v[0], v[1], v[2], v[3]};
+      const auto d = __builtin_amdgcn_raw_buffer_load_b64(rr, (uint32_t)(grow * 8 + 64 * q), 0, 0);
+      ra[q] = __builtin_bit_cast(double, d);
+    }
+  };
+#else
   auto load_ids = [&](const Batch &x, int32_t (&it)[Q]) __attribute__((always_inline)) {
     if (x.r1 > x.r0) {
 #pragma unroll
@@ -1253,6 +1291,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       ra[q] = a.ra_edge[in ? r : 0];
     }
   };
+
+#endif
 
   // ---- top-K state of the current user (MODE_TOPK), loaded at its first batch
   constexpr bool kTwo = M > 2;  // k > 64: the list spans two registers per lane
@@ -2073,6 +2113,8 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
              "lg_spread_tile_resource_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile,
              "lg_spread_tile_resource_f64: tile %d / width %d", tile, width);
+  LG_REQUIRE(null_row >= 0 && null_row < (1 << 25) - 1,
+             "tile walk: %d items exceed the 32-bit line offsets", null_row);
   if (n_users == 0) return LG_OK;
   WalkArgs a{};
   a.user_rowptr = user_rowptr;
@@ -2168,6 +2210,8 @@ extern "C" int lg_spread_tile_resource_topk_f64(
              "bound per lane), got %d", width);
   LG_REQUIRE(!ex_rowptr == !ex_col && !ex_rowptr == !ex_cur,
              "lg_spread_tile_resource_topk_f64: ex_rowptr/ex_col/ex_cur go together");
+  LG_REQUIRE(null_row >= 0 && null_row < (1 << 25) - 1,
+             "tile walk: %d items exceed the 32-bit line offsets", null_row);
   if (n_users == 0) return LG_OK;
   WalkArgs a{};
   a.user_rowptr = user_rowptr;
