@@ -1079,11 +1079,14 @@ struct WalkArgs {
             // 64 = no exact G score, 128 = no G candidates
 };
 
-// per wave: acc[tile], the overflow list (decode) and the user's embedding (MODE_TOPK with
+// accumulator columns per wave: the tile rounded up to whole 512-column scan steps
+__host__ __device__ constexpr int acc_cols(int tile) { return (tile + 511) / 512 * 512; }
+
+// per wave: acc[acc_cols(tile)], the overflow list (decode) and the user's embedding (MODE_TOPK with
 // D > 0; the running list itself lives in registers)
 template <int MODE, int D, int M>
 __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
-  return ((size_t)tile * 8 + (size_t)kOvfList * 12 +
+  return ((size_t)acc_cols(tile) * 8 + (size_t)kOvfList * 12 +
           (MODE == MODE_TOPK && D > 0 ? (size_t)D * 4 : 0) + 15) &
          ~(size_t)15;
 }
@@ -1186,8 +1189,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   const uint32_t acc_base = (uint32_t)(uintptr_t)(lds_f64 *)acc;
   // the lane's dummy word for empty slots: its entry of the overflow list (rewritten before
   // every use; adding 0.0 leaves it unchanged meanwhile)
-  const uint32_t dummy_addr = acc_base + 8u * (uint32_t)(tile + lane);
-  double *ovl_ra = acc + tile;  // overflow list (decode)
+  const uint32_t dummy_addr = acc_base + 8u * (uint32_t)(acc_cols(tile) + lane);
+  double *ovl_ra = acc + acc_cols(tile);  // overflow list (decode)
   uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
   float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);  // the user's row (D > 0)
   (void)us;
@@ -1202,7 +1205,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, o));
   if (lane == 0) s_red[wave] = rmax;
-  for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
+  for (int j = lane; j < acc_cols(tile); j += 64) acc[j] = 0.0;
   __syncthreads();
   rmax = 0.0;
   for (int w = 0; w < nw; ++w) rmax = fmax(rmax, s_red[w]);
@@ -1589,11 +1592,9 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #pragma unroll
           for (int pp = 0; pp < 2; ++pp) {
             const int j = c0 + 256 * hh + 4 * lane + 2 * pp;
-            double2 x = double2{neg_inf<double>(), neg_inf<double>()};
-            if (j < tile) {
-              x = *reinterpret_cast<const double2 *>(acc + j);
-              *reinterpret_cast<double2 *>(acc + j) = zero2;
-            }
+            // (acc holds whole 512-column steps: no bounds branch, the 4 reads go out together)
+            const double2 x = *reinterpret_cast<const double2 *>(acc + j);
+            *reinterpret_cast<double2 *>(acc + j) = zero2;
             sv[4 * hh + 2 * pp] = j < a.width ? x.x : neg_inf<double>();
             sv[4 * hh + 2 * pp + 1] = j + 1 < a.width ? x.y : neg_inf<double>();
           }
@@ -1672,7 +1673,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           }
         }
       }
-      for (int j = a.width + lane; j < tile; j += 64) acc[j] = 0.0;  // (never touched)
       if (dirty) {
         if (lane < k) {
           a.io_val[u * k + lane] = I0 != kPadId ? L0 : neg_inf<double>();
