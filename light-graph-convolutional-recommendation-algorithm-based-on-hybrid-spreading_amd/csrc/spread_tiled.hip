@@ -1706,7 +1706,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     if (c.first) load_user(c.u);
     decode(c, wc, rc);
     if (c.r1 >= c.e) finish_user(c.u);
-    if (n2.u < n_users) load_rows(n2, it2, wc, rc);  // batch t+2 into the freed registers
+    // batch t+2 into the freed registers (issued before the scan instead: 1.5 % slower)
+    if (n2.u < n_users) load_rows(n2, it2, wc, rc);
     const Batch n3 = n2.u < n_users ? next_batch(n2) : Batch{n_users, 0, 0, 0, false};
     if (n3.u < n_users) load_ids(n3, it2);
     c = d;
