@@ -385,10 +385,17 @@ __global__ __launch_bounds__(256) void k_group_bound(const int64_t *__restrict__
   int64_t s[kGroupMax];
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) s[t] = 0;
-  for (int64_t e = item_rowptr[i] + lane; e < item_rowptr[i + 1]; e += 64) {
-    const uint4 c = counts[item_users[e]];
+  // two 64-user chunks per iteration: both gathers in flight together
+  const int64_t e1 = item_rowptr[i + 1];
+  for (int64_t b = item_rowptr[i]; b < e1; b += 128) {
+    const int64_t e = b + lane;
+    const bool in0 = e < e1, in1 = e + 64 < e1;
+    const int32_t v0 = in0 ? item_users[e] : 0, v1 = in1 ? item_users[e + 64] : 0;
+    uint4 c0{0u, 0u, 0u, 0u}, c1{0u, 0u, 0u, 0u};
+    if (in0) c0 = counts[v0];
+    if (in1) c1 = counts[v1];
 #pragma unroll
-    for (int t = 0; t < kGroupMax; ++t) s[t] += count_of(c, t);
+    for (int t = 0; t < kGroupMax; ++t) s[t] += count_of(c0, t) + count_of(c1, t);
   }
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) {
@@ -473,13 +480,27 @@ __global__ __launch_bounds__(256) void k_group_rows(
   for (int t = 0; t < kGroupMax; ++t) n[t] = 0;
   uint32_t farbits = 0;
   const int64_t e1 = item_rowptr[i + 1];
-  for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
-    const int64_t e = e0 + lane;
-    uint4 rc{0u, 0u, 0u, 0u};
-    int32_t v = 0;
+  // the next chunk's users and records are gathered while this chunk is written
+  uint4 rcn{0u, 0u, 0u, 0u};
+  int32_t vn = 0;
+  {
+    const int64_t e = item_rowptr[i] + lane;
     if (e < e1) {
-      v = item_users[e];
-      rc = rec[v];
+      vn = item_users[e];
+      rcn = rec[vn];
+    }
+  }
+  for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
+    const uint4 rc = rcn;
+    const int32_t v = vn;
+    if (e0 + 64 < e1) {
+      const int64_t e = e0 + 64 + lane;
+      rcn = uint4{0u, 0u, 0u, 0u};
+      vn = 0;
+      if (e < e1) {
+        vn = item_users[e];
+        rcn = rec[vn];
+      }
     }
     const uint32_t nu = rc.x & 0xFFu;  // the user's items in the group
     const bool longu = nu > (uint32_t)kRecItems;
