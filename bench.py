@@ -453,8 +453,13 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
         per_user = 2 * k * 16 + st.get("qstride", 0) + 4 * st.get("nch", 0) + 16
         alg = (st["w_bytes"] + 12 * st["user_items"] + per_user * st["users"] * nl) / nl
         ms = st["t_walk_ms"] / nl
+        traffic, traffic_src = (None, {"status": "PMC record is for the 1M-item tile walk"})
+        if (U, I) == (1_000_000, 1_000_000) and tile == 2048:
+            traffic, traffic_src = load_traffic("c5-d64", 1, "spread_tiled.hip",
+                                                "c5-d64/spread_walk")
         walk = {"bound": "hbm", "achieved": alg / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg / ms / 1e6 / HBM_PEAK_GBS, "traffic": None,
+                "frac": alg / ms / 1e6 / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "lg_spread_tile_resource_topk_f64", "avg_launch_ms": ms,
                 "alg_bytes_per_launch": alg, "launches": nl,
                 "paths_per_launch": st["w_paths"] / nl,
@@ -505,25 +510,28 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
     return res
 
 
-def load_traffic(workload, world):
-    """roofline.traffic: HBM bytes per SpMM launch from the PMC pass recorded in
+def load_traffic(workload, world, src_name="spmm.hip", key=None):
+    """roofline.traffic: HBM bytes per launch of a kernel from the PMC pass recorded in
     profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH x 2 per the
-    gfx950 correction; scripts/profile.sh + scripts/pmc_summary.py). The entry is used only
-    if the kernel source it was measured on (sha256 of csrc/spmm.hip) is the one built now;
+    gfx950 correction; K1: scripts/profile.sh + scripts/pmc_summary.py under
+    "<workload>/n<world>", the K3s walk: scripts/gpu_r02_walk_traffic.sh +
+    scripts/walk_traffic_summary.py under "c5-d64/spread_walk"). The entry is used only if
+    the kernel source it was measured on (sha256 of csrc/<src_name>) is the one built now;
     otherwise traffic is null and the reason is reported."""
     import hashlib
-    src = os.path.join(PKG, "csrc", "spmm.hip")
+    src = os.path.join(PKG, "csrc", src_name)
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    key = key or f"{workload}/n{world}"
     try:
         d = json.load(open(path))
     except Exception:
         return None, {"status": "no PMC record", "kernel_sha": sha}
-    e = d.get(f"{workload}/n{world}")
+    e = d.get(key)
     if e is None:
-        return None, {"status": f"no PMC record for {workload}/n{world}", "kernel_sha": sha}
+        return None, {"status": f"no PMC record for {key}", "kernel_sha": sha}
     if e.get("kernel_sha") != sha:
-        return None, {"status": "stale: recorded on another spmm.hip",
+        return None, {"status": f"stale: recorded on another {src_name}",
                       "recorded_sha": e.get("kernel_sha"), "kernel_sha": sha,
                       "source": e.get("source")}
     return float(e["hbm_bytes_per_launch"]), {"status": "measured", "kernel_sha": sha,
