@@ -1616,9 +1616,16 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             // (acc holds whole 512-column steps: no bounds branch, the 4 reads go out together)
             const double2 x = *reinterpret_cast<const double2 *>(acc + j);
             *reinterpret_cast<double2 *>(acc + j) = zero2;
-            sv[4 * hh + 2 * pp] = j < a.width ? x.x : neg_inf<double>();
-            sv[4 * hh + 2 * pp + 1] = j + 1 < a.width ? x.y : neg_inf<double>();
+            sv[4 * hh + 2 * pp] = x.x;
+            sv[4 * hh + 2 * pp + 1] = x.y;
           }
+        if (c0 + 512 > a.width) {  // the last step of a partial tile: columns past the width
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int j = c0 + 256 * (t >> 2) + 4 * lane + (t & 3);
+            if (j >= a.width) sv[t] = neg_inf<double>();
+          }
+        }
         double sc0 = 0.0, sc1 = 0.0;
         if constexpr (D > 0) {
           sc0 = __shfl(sc_v, ((c0 + 4 * lane) >> 6) & 63);
