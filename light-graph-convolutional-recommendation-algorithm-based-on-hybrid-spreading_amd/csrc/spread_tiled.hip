@@ -475,7 +475,7 @@ __global__ __launch_bounds__(256) void k_group_rows(
     if (has_ovf && lane < 4) ov[ou * 4 + lane] = lane == 0 ? (uint32_t)n_units : 0u;
     for (int64_t p = nb + lane; p < cap; p += 64) put_slot(line, ov, ou, p, 0u);
   }
-  int64_t n[kGroupMax];
+  uint32_t n[kGroupMax];  // pairs written so far per tile (P rows: <= vthr < 2^16)
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) n[t] = 0;
   uint32_t farbits = 0;
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void k_group_rows(
               const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
               jr = ((k & 1) ? wd >> 16 : wd) & 0x1FFFu;
             }
-            put_slot(line, ov, ou, n[t] + pb + q, (cl << 16) | jr);
+            put_slot(line, ov, ou, (int64_t)(n[t] + pb + q), (cl << 16) | jr);
           }
           if (ct && cl >= (uint32_t)kInvTab) farbits |= 1u << t;
           n[t] += tot;
