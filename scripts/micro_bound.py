@@ -1,0 +1,64 @@
+"""Where the score-bound kernel's time goes at C5 (1M users, one 2048-column tile, D = 64):
+lg_score_chunk_bound with the per-column q bytes, with gb only (no q), and a plain 2 GB
+device write (torch fill_) as the HBM write ceiling for the q bytes. Prints one JSON line.
+Usage: python scripts/micro_bound.py [--users 1000000] [--dim 64]"""
+import argparse
+import json
+import os
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [R, os.path.join(R, "light-graph-convolutional-recommendation-algorithm-based-on-hybrid-spreading_amd")]
+import torch  # noqa: E402
+
+from lgcnhs import ops  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--users", type=int, default=1_000_000)
+ap.add_argument("--items", type=int, default=1_000_000)
+ap.add_argument("--dim", type=int, default=64)
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(1)
+eu = torch.randn(a.users, a.dim, device=dev, generator=g) * 0.1
+ei = torch.randn(a.items, a.dim, device=dev, generator=g) * 0.1
+ub, un = ops.bound_operands(eu)
+ib, inn = ops.bound_operands(ei)
+T = 2048
+gb = torch.empty(a.users * (T // 64), dtype=torch.float32, device=dev)
+q = torch.empty(a.users, T, dtype=torch.uint8, device=dev)
+s = torch.cuda.current_stream(dev)
+
+
+def timed(fn):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for r in range(a.reps):
+        fn(r)
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / a.reps
+
+
+def with_q(r=0):
+    ops.chunk_bounds(ub, un, ib, inn, a.dim, (r * T) % (a.items - T), T, out=gb, qout=q)
+
+
+def gb_only(r=0):
+    ops.chunk_bounds(ub, un, ib, inn, a.dim, (r * T) % (a.items - T), T, out=gb)
+
+
+def fill(r=0):
+    q.fill_(r & 255)
+
+
+res = {"users": a.users, "tile": T, "dim": a.dim,
+       "with_q_ms": timed(with_q), "gb_only_ms": timed(gb_only), "fill_q_ms": timed(fill)}
+qbytes = a.users * T
+res["fill_GBps"] = qbytes / res["fill_q_ms"] / 1e6
+res["with_q_write_GBps"] = (qbytes + gb.numel() * 4) / res["with_q_ms"] / 1e6
+res["mfma_TFLOPs_with_q"] = 2 * a.users * T * a.dim / res["with_q_ms"] / 1e9
+print(json.dumps(res), flush=True)
