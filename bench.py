@@ -22,7 +22,9 @@ Phases after the timed steps (each reported in its own key of the same JSON line
   cpu_baseline*  the reference's op sequences (oracle restatement) on host cores, bounded
           samples (skip with --no-cpu-baseline).
 
-Run: python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
+Run: python bench.py [--gpus N --steps K --warmup W]. N > 1: one process per GPU, either
+under the caller's torch.distributed.run (WORLD_SIZE must equal N) or started here as a child
+torch.distributed.run when WORLD_SIZE is unset.
 """
 from __future__ import annotations
 
@@ -30,6 +32,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -538,6 +542,50 @@ def load_traffic(workload, world, src_name="spmm.hip", key=None):
                                                "source": e.get("source")}
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int | None:
+    """--gpus N without a torch.distributed launcher around us: start N ranks as a CHILD
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and return its exit
+    code; rank 0's JSON line reaches our stdout through the inherited pipe. Nothing here
+    touches the GPU (the parent never initialises HIP, and never execs). Returns None when
+    this process is itself a rank (WORLD_SIZE set) or N == 1. A launcher whose WORLD_SIZE
+    differs from --gpus is an error: the line would report the wrong n_gpus."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            log(f"bench: WORLD_SIZE={env_world} but --gpus {args.gpus}")
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(world: int, rank: int) -> None:
+    """--launch-check: the rank plumbing alone (process group, one all-reduce, rank 0's
+    JSON line), no GPU work; what the CPU tests drive through launch_ranks()."""
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "launch-check", "n_gpus": world,
+                          "ranks_seen": int(t.item())}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -563,13 +611,23 @@ def main():
     ap.add_argument("--layout", default="bipartite", choices=["bipartite", "rows"],
                     help="N>1 row sharding: users and items sharded separately with "
                          "cross-layer overlap (bipartite) or contiguous node rows (rows)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank plumbing only (process group + one all-reduce), no GPU work")
     args = ap.parse_args()
 
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local = 0
+    if args.launch_check:
+        if world > 1:
+            dist.init_process_group(args.backend if args.backend != "nccl" else "gloo")
+        launch_check(world, rank)
+        return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)

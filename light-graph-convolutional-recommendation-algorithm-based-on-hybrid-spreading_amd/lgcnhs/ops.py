@@ -760,6 +760,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
             stats["t_bounds_ms"] = stats.get("t_bounds_ms", 0.0) + sum(e[1].elapsed_time(e[2]) for e in evs)
             stats["t_walk_ms"] = stats.get("t_walk_ms", 0.0) + sum(e[2].elapsed_time(e[3]) for e in evs)
             stats["walk_launches"] = stats.get("walk_launches", 0) + len(evs)
+            stats["walk_ms_list"] = stats.get("walk_ms_list", []) + [e[2].elapsed_time(e[3]) for e in evs]
             stats["user_items"] = stats.get("user_items", 0) + len(evs) * int(
                 A.by_user.rowptr[u1] - A.by_user.rowptr[u0])
             stats["users"] = n

@@ -44,3 +44,8 @@ for rep in range(a.reps):
           + (f"  paths {st.get('w_paths', 0):.3e} bytes {st.get('w_bytes', 0):.3e}"
              f"  build {st.get('t_build_ms', 0):.1f} ms bounds {st.get('t_bounds_ms', 0):.1f} ms"
              f" walk {st.get('t_walk_ms', 0):.1f} ms" if st else ""), flush=True)
+    if st.get("walk_ms_list"):
+        wl = st["walk_ms_list"]
+        h = len(wl) // 3
+        print(f"  walk ms per tile: first {h} {sum(wl[:h]) / max(1, h):.3f}, "
+              f"rest {sum(wl[h:]) / max(1, len(wl) - h):.3f}", flush=True)

@@ -1,0 +1,44 @@
+"""bench.py --gpus N starts N ranks itself when no launcher set WORLD_SIZE (a child
+torch.distributed.run, never an exec), and refuses a launcher whose world differs from N.
+CPU only: --launch-check runs the rank plumbing (gloo process group, one all-reduce, rank 0's
+JSON line) without GPU work."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env):
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=240, cwd=REPO)
+
+
+def test_gpus_2_launches_two_ranks():
+    p = _run(["--gpus", "2", "--backend", "gloo", "--launch-check"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
+
+
+def test_gpus_1_stays_single_process():
+    p = _run(["--gpus", "1", "--launch-check"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+    assert "launching" not in p.stderr
+
+
+def test_world_size_must_match_gpus():
+    p = _run(["--gpus", "2", "--launch-check"], _env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode != 0
+    assert "WORLD_SIZE=3" in p.stderr
