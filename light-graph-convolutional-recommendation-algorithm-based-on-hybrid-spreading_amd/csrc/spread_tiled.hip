@@ -1032,41 +1032,13 @@ __device__ __forceinline__ float chain_score(const float *us, const float *__res
 //            only those columns get rb_j and (with G) the exact chain score. Ids grow along
 //            the walk, so "beats" is v > tau (a tie loses to the older, smaller id).
 constexpr int MODE_F = 0, MODE_TOPK = 1;
-#ifndef LG_BUFFER_LOADS
-#define LG_BUFFER_LOADS 1  // batch loads through buffer descriptors (32-bit offsets)
-#endif
-#ifndef LG_BRANCHLESS
-#define LG_BRANCHLESS 1  // empty slots add 0.0 to a per-lane dummy (no branch per slot)
-#endif
-#ifndef LG_WALK_COUNT
-#define LG_WALK_COUNT 0  // measurement build: event counters of the top-K scan
-#endif
-#if LG_WALK_COUNT
-// [0] 512-column scan steps with a pre-screen pass, [1] pre-screen passes, [2] lanes x
-// drain rounds (/64 = rounds), [3] exact-score candidates, [4] lanes x rounds with an exact
-// score (/64), [5] insertions (/64); counted per lane with wave-level atomics
-__device__ unsigned long long g_walk_cnt[8];
-__device__ __forceinline__ void walk_count(int k, unsigned long long v) {
-  if (v) atomicAdd(&g_walk_cnt[k], v);
-}
-__device__ __forceinline__ void walk_count_lanes(int k, int v) {
-  uint64_t s = (uint64_t)v;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane_id() == 0 && s) atomicAdd(&g_walk_cnt[k], (unsigned long long)s);
-}
-#endif
 constexpr int kWalkQ = 8;       // line loads per lane per batch: 8 rows each, 64 rows
 constexpr int kBatchRows = 8 * kWalkQ;
 constexpr int kOvfList = kBatchRows;
-#ifndef LG_DECODE_PHASE
-#define LG_DECODE_PHASE 4
-#endif
-constexpr int kDecodePhase = LG_DECODE_PHASE;
+constexpr int kDecodePhase = 4;  // lines whose class reads precede their adds
 // q dwords per lane loaded with the user's first batch (256 columns each), then streamed
 // kQPre / 2 scan iterations ahead (4 and 8 measured no faster than 2: 3.22 / 3.33 vs 3.20 s)
 constexpr int kQPre = 2;
-  // lines whose class reads precede their adds
 static_assert(kWalkQ % kDecodePhase == 0, "decode phase must divide the batch's line loads");
 
 struct WalkArgs {
@@ -1095,9 +1067,6 @@ struct WalkArgs {
   int k, first;
   double *io_val;
   int64_t *io_idx;
-  int dbg;  // measurement knob (LGCNHS_WALK_DBG): 1 = no LDS atomics, 2 = no decode, 4 = no
-            // scan, 16 = plain LDS stores, 32 = atomics to conflict-free addresses,
-            // 64 = no exact G score, 128 = no G candidates
 };
 
 // accumulator columns per wave: the tile rounded up to whole 512-column scan steps
@@ -1126,12 +1095,6 @@ __device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
 typedef __attribute__((address_space(3))) double lds_f64;
 __device__ __forceinline__ double slot_inv_fast(uint32_t s) {
   return *(const lds_f64 *)(uintptr_t)(s >> 13);
-}
-__device__ __forceinline__ void slot_add_fast(uint32_t acc_base, uint32_t s, double v) {
-  uint32_t addr;
-  asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(addr) : "v"(s), "v"(acc_base));
-  __hip_atomic_fetch_add((lds_f64 *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // Branch-free form: an empty slot (s == 0, value 0) adds its 0.0 to the lane's own dummy
 // word instead (no exec-mask branch per slot; the dummies are lane-distinct: no conflicts).
@@ -1258,7 +1221,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     return new_user();
   };
   // item ids of a batch's rows (lanes of one 8-lane group: one row)
-#if LG_BUFFER_LOADS
   // Buffer loads with 32-bit offsets: a batch's item ids and ra through a descriptor based
   // at its first row (lane offsets are per-lane constants + immediates; rows past the batch
   // are out of range and read 0), the lines through one descriptor for the tile.
@@ -1292,31 +1254,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       ra[q] = __builtin_bit_cast(double, d);
     }
   };
-#else
-  auto load_ids = [&](const Batch &x, int32_t (&it)[Q]) __attribute__((always_inline)) {
-    if (x.r1 > x.r0) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int64_t r = x.r0 + 8 * q + grow;
-        it[q] = a.user_items[r < x.r1 ? r : x.r0];
-      }
-    }
-  };
-  // lines and ra of a batch (rows past r1 read the zero line)
-  auto load_rows = [&](const Batch &x, const int32_t (&it)[Q], uint4 (&w)[Q], double (&ra)[Q])
-      __attribute__((always_inline)) {
-    // (every load group is issued even past a short last batch: skipping them with a
-    // uniform branch measured 40 % slower -- the branches cost the loads their overlap)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int64_t r = x.r0 + 8 * q + grow;
-      const bool in = r < x.r1;
-      w[q] = a.lines[(int64_t)(in ? it[q] : a.null_row) * 8 + gh];
-      ra[q] = a.ra_edge[in ? r : 0];
-    }
-  };
-
-#endif
 
   // ---- top-K state of the current user (MODE_TOPK), loaded at its first batch
   constexpr bool kTwo = M > 2;  // k > 64: the list spans two registers per lane
@@ -1367,38 +1304,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   };
 
   // ---- decode one batch into acc
-  double dbg_sink = 0.0;
   auto decode = [&](const Batch &x, uint4 (&w)[Q], const double (&ra)[Q])
       __attribute__((always_inline)) {
-    if (a.dbg & 2) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) dbg_sink += (double)(w[q].x ^ w[q].y ^ w[q].z ^ w[q].w) * ra[q];
-      return;
-    }
-    if (a.dbg & 1) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const uint32_t s0 = w[q].x & hmask;
-        dbg_sink += s_inv[s0 >> 16] * ra[q] + s_inv[w[q].y >> 16] * ra[q] +
-                    s_inv[w[q].z >> 16] * ra[q] + s_inv[w[q].w >> 16] * ra[q];
-      }
-      return;
-    }
-    if (a.dbg & 48) {  // 16: plain stores instead of atomics; 32: atomics to acc[lane]
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const uint32_t sv[4] = {w[q].x & hmask, w[q].y, w[q].z, w[q].w};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const double v = s_inv[sv[t] >> 16] * ra[q];
-          if (sv[t]) {
-            if (a.dbg & 16) acc[sv[t] & 0xFFFFu] = v;
-            else lds_add(acc, (uint32_t)(lane * 4 + t), v);
-          }
-        }
-      }
-      return;
-    }
     uint32_t hdr = 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) hdr |= w[q].x & ~hmask;  // the group heads' headers
@@ -1424,15 +1331,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           const uint32_t sv[4] = {w[q0 + q].x & hmask, w[q0 + q].y, w[q0 + q].z, w[q0 + q].w};
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-#if LG_DBG_SEQ_ADDS  // measurement build: the same adds at conflict-free addresses
-            if (sv[t]) lds_add(acc, (uint32_t)(lane * 4 + t), inv[q][t] * ra[q0 + q]);
-#else
-#if LG_BRANCHLESS
             slot_add_nobranch(acc_base, dummy_addr, sv[t], inv[q][t] * ra[q0 + q]);
-#else
-            if (sv[t]) slot_add_fast(acc_base, sv[t], inv[q][t] * ra[q0 + q]);
-#endif
-#endif
         }
       }
     } else {
@@ -1484,10 +1383,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   // ---- the user's tile of F: written out (MODE_F) or merged into its top-K list
   auto finish_user = [&](int64_t u) __attribute__((always_inline)) {
     wave_sync();
-    if (a.dbg & 4) {
-      if (dbg_sink == 1.2345) acc[lane] = dbg_sink;  // keeps the debug sums alive
-      return;
-    }
     if constexpr (MODE == MODE_F) {
       double *row = a.F + u * a.ldf;
       for (int j = lane; j < tile; j += 64) {
@@ -1644,13 +1539,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           }
           mask |= pre ? 1u << t : 0u;
         }
-#if LG_WALK_COUNT
-        {
-          const bool any = __ballot(mask != 0) != 0;
-          if (lane == 0) walk_count(0, any ? 1 : 0);
-        }
-        walk_count_lanes(1, __popc(mask));
-#endif
         while (__ballot(mask != 0)) {
           const bool has = mask != 0;
           const int t = has ? __ffs(mask) - 1 : 0;
@@ -1665,29 +1553,18 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
                               __shfl(bq_v, (j >> 6) & 63);
             const bool cand = has && bq * f > tau;
-#if LG_WALK_COUNT
-            walk_count_lanes(2, 1);
-            walk_count_lanes(3, cand ? 1 : 0);
-#endif
             if (__ballot(cand)) {
-#if LG_WALK_COUNT
-              walk_count_lanes(4, 1);
-#endif
               need_us();
               double v = 0.0;
               const int item = a.item_begin + j;
               if (cand) {
-                if (a.dbg & 64) v = f;  // (measurement: no exact score)
-                else v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * f;
+                v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * f;
               }
               uint64_t bal = __ballot(cand && before(v, item, tau, tau_id));
               while (bal) {
                 const int l = __ffsll((long long)bal) - 1;
                 bal &= bal - 1;
                 insert1(__shfl(v, l), __shfl(item, l));
-#if LG_WALK_COUNT
-                walk_count_lanes(5, 1);
-#endif
               }
             }
           } else {
@@ -1760,13 +1637,8 @@ static void launch_tile_topk_v(int M, const double *F, int64_t ldf, int64_t n_ro
   // list is compacted once it holds more than S-16 entries, so the first span of a walk,
   // where most columns enter, keeps S=64), 48 KiB (M=2), 96 KiB (M=4). Measured per 4096-
   // column span at 1M users: S=40 8.4-8.6 ms vs S=64 8.8-9.1 ms after the first spans,
-  // 26.4 vs 16.7 ms on the first. LGCNHS_TILE_TOPK_S64=1 (A/B knob) keeps S=64 throughout.
-  static int s64 = -1;
-  if (s64 < 0) {
-    const char *e = getenv("LGCNHS_TILE_TOPK_S64");
-    s64 = e ? atoi(e) : 0;
-  }
-  if (M == 1 && k <= 24 && !first && !s64) {
+  // 26.4 vs 16.7 ms on the first.
+  if (M == 1 && k <= 24 && !first) {
     const unsigned b = (unsigned)((n_rows + 63) / 64);
     k_tile_topk<D, 2, 1, VEC, 40><<<b, 128, 0, s>>>(F, ldf, n_rows, j0, n_cols, eu, ei,
                                                     ex_rowptr, ex_col, drop, k, first, io_val,
@@ -2077,15 +1949,6 @@ extern "C" int lg_spread_group_rows_f64(
   return launch_status("lg_spread_group_rows_f64");
 }
 
-static int walk_dbg() {  // measurement knob only: results are wrong when set
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("LGCNHS_WALK_DBG");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 static int n_cus() {
   static int n_cu = 0;
   if (n_cu == 0) {
@@ -2116,17 +1979,6 @@ static int launch_walk(const WalkArgs &a, hipStream_t s) {
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   const size_t lds = shared + (size_t)nw * per;
   k_tile_walk<MODE, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
-#if LG_WALK_COUNT
-  static int launches = 0;
-  if (++launches % 50 == 0 || a.item_begin + a.width >= a.null_row) {
-    unsigned long long h[8];
-    hipStreamSynchronize(s);
-    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_walk_cnt), sizeof(h));
-    fprintf(stderr, "[walk count] launches %d users %lld: steps_with_pass %llu passes %llu "
-            "rounds %llu cands %llu cand_rounds %llu inserts %llu\n", launches,
-            (long long)a.n_users, h[0], h[1], h[2] / 64, h[3], h[4] / 64, h[5] / 64);
-  }
-#endif
   return LG_OK;
 }
 
@@ -2160,7 +2012,6 @@ extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
   a.g_inv = inv_cls;
   a.F = F;
   a.ldf = ldf;
-  a.dbg = walk_dbg();
   const int st = launch_walk<MODE_F, 0, 1>(a, (hipStream_t)stream);
   if (st != LG_OK) return st;
   return launch_status("lg_spread_tile_resource_f64");
@@ -2268,7 +2119,6 @@ extern "C" int lg_spread_tile_resource_topk_f64(
   a.first = first;
   a.io_val = io_val;
   a.io_idx = io_idx;
-  a.dbg = walk_dbg();
   hipStream_t s = (hipStream_t)stream;
   const int M = k <= 64 ? 2 : 4;
   int st;
