@@ -1,6 +1,8 @@
 """Configuration with the keys the reference's hot path reads (reference const.py:11-518):
 ``cfg.DATA_SET``, ``cfg.MODEL["name" | "HyperParameter" | "save_path"]``,
-``cfg.RECOMMEND["k" | "save_path"]``, ``cfg.LOG``, ``cfg.PREPROCESSING["save_path"]``.
+``cfg.RECOMMEND["k" | "save_path" | "target_user"]``, ``cfg.LOG``, ``cfg.PREPROCESSING[...]``
+(every key of the reference's, including the ETL keys ``dataset_path_dict``, ``columns_map``,
+``quantile`` and ``vector_size`` that main.py's cache-miss branch and processing/* read).
 
 Selection is by environment variables instead of editing module globals
 (reference const.py:494-518): LGCNHS_ENV (dev|prod), LGCNHS_DATASET (movielens|douban),
@@ -37,6 +39,31 @@ _HP = {
 }
 
 
+# per-dataset ETL keys (reference const.py:81-95 defaults, :202-244 dev, :446-488 prod)
+_DATASET_DIRS = {("dev", "movielens"): "I:/Workspace/data/ml-100k/",
+                 ("dev", "douban"): "I:/Workspace/data/douban/",
+                 ("prod", "movielens"): "/data/datasets/recommend/ml-100k/",
+                 ("prod", "douban"): "/data/datasets/recommend/douban/"}
+_ETL = {
+    "movielens": {
+        "files": {"users": "u.user", "items": "u.item", "rating": "u.data",
+                  "occupation": "u.occupation"},
+        "columns_map": {"user_id": "user", "item_id": "item", "rating": "rating",
+                        "rating_time": "timestamp"},
+        "quantile": {"start": 1, "end": 0},
+        "vector_size": {"title": 5, "content": 20},
+    },
+    "douban": {
+        "files": {"users": "users.csv", "items": "movies.csv", "rating": "ratings.csv"},
+        "columns_map": {"user_id": "USER_MD5", "item_id": "MOVIE_ID", "rating": "RATING",
+                        "rating_time": "RATING_TIME"},
+        "quantile": {"start": 0.991, "end": 0.99},
+        "vector_size": {"title": 3, "content": 20},
+        "target_user": "1a76e2591cd2f3740ccb7f198dace22a",
+    },
+}
+
+
 class Config:
     def __init__(self, env: str = "dev", dataset: str = "movielens",
                  model: str = "SpreadLightGCNOpti", root: str | None = None) -> None:
@@ -45,13 +72,24 @@ class Config:
         base = os.path.join(root, dataset)
         self.ENV = env
         self.DATA_SET = dataset
-        self.PREPROCESSING = {"seed": 42, "save_path": base + "/preprocess/",
-                              "split_percentage": [0.2, 0.5]}
+        etl = _ETL.get(dataset, {})
+        ddir = _DATASET_DIRS.get((env, dataset), "")
+        self.PREPROCESSING = {
+            "seed": 42,
+            "dataset_path_dict": {k: ddir + f for k, f in etl.get("files", {}).items()},
+            "save_path": base + "/preprocess/",
+            "vector_size": dict(etl.get("vector_size", {})),
+            "columns_map": dict(etl.get("columns_map", {})),
+            "quantile": dict(etl.get("quantile", {"start": 1, "end": 0})),
+            "split_percentage": [0.2, 0.5],
+        }
         self.LOG = {"file_path": base + "/log/"}
         self.MODEL = {"name": model, "HyperParameter": dict(_HP.get((env, model), {})),
                       "save_path": base + "/model/"}
         self.EVALUATION = {"save_path": base + "/evaluation/"}
         self.RECOMMEND = {"k": 10 if env == "dev" else 100, "save_path": base + "/recommend/"}
+        if "target_user" in etl:
+            self.RECOMMEND["target_user"] = etl["target_user"]
         self.PICTURES = {"save_path": base + "/pictures/"}
 
 

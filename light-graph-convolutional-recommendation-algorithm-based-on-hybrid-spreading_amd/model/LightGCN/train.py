@@ -3,8 +3,9 @@
 forward/backward through the HIP propagation, and every ``epoch_per_eval`` epochs the
 reference's validation block (:147-180): val loss on the val adjacency, train-masked top-k
 (model/LightGCN/evaluation.py), P/R/F1/NDCG against the val positives and H/I diversity.
-The per-eval metrics are written to the reference's ``<k>_val_metrics.csv`` (plots are not
-drawn); the model is saved as a state_dict (loadable with weights_only=True)."""
+The per-eval metrics are written to the reference's ``<k>_val_metrics.csv`` and drawn as its
+curves (:205-221, utils.picture.plotMetric); the model is saved as a state_dict (loadable with
+weights_only=True)."""
 import os
 
 import pandas as pd
@@ -112,8 +113,36 @@ def train_model(model, user_num: int, item_num: int, train_edge_index, val_edge_
         df = pd.DataFrame(state.rows)
         df["iters"] = [i * hp["epoch_per_eval"] for i in range(len(df))]
         df.to_csv(out, index=False)
+        plot_curves(df, cfg.PICTURES["save_path"] + f"{name}_{k}")
     model.val_metrics = None if state is None else list(state.rows)
     return model
+
+
+def plot_curves(df: pd.DataFrame, save_path: str) -> None:
+    """The reference's training curves (:205-221): train / validation loss, then one plot per
+    validation metric, as <save_path>_<metric>.png."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    from utils.picture import plotMetric
+    it = df["iters"].tolist()
+    fig = plt.figure()
+    plt.plot(it, df["train_loss"].tolist(), label="train")
+    plt.plot(it, df["val_loss"].tolist(), label="validation")
+    plt.xlabel("iteration")
+    plt.ylabel("loss")
+    plt.title("training and validation loss curves")
+    plt.legend()
+    plt.savefig(save_path + "_loss_curves.png")
+    plt.close(fig)
+    for col, label, suffix in (("val_precision", "precision", "precision"),
+                               ("val_recall", "recall", "recall"),
+                               ("val_f1", "F1-score", "F1-score"),
+                               ("val_ndcg", "NDCG", "NDCG"), ("val_H", "H", "H"),
+                               ("val_I", "I", "I")):
+        plotMetric(it, df[col].tolist(), "iteration", label, f"{label} curves",
+                   save_path + f"_{suffix}.png")
 
 
 @calTimes(logger, "模型训练完成")

@@ -35,7 +35,7 @@ for rep in range(a.reps):
     torch.cuda.synchronize()
     t = time.time()
     st = {}
-    ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile, fused=not a.unfused,
+    vals, idxs = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile, fused=not a.unfused,
                           items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30,
                           stats=st if rep == 0 else None, count_paths=a.count, **kw)
     torch.cuda.synchronize()
@@ -44,6 +44,9 @@ for rep in range(a.reps):
           + (f"  paths {st.get('w_paths', 0):.3e} bytes {st.get('w_bytes', 0):.3e}"
              f"  build {st.get('t_build_ms', 0):.1f} ms bounds {st.get('t_bounds_ms', 0):.1f} ms"
              f" walk {st.get('t_walk_ms', 0):.1f} ms" if st else ""), flush=True)
+    h = (idxs.to(torch.float64) * torch.arange(1, 21, device=dev, dtype=torch.float64)).sum()
+    print(f"  lists checksum {float(h):.17g} values sum {float(vals[torch.isfinite(vals)].sum()):.17g}",
+          flush=True)
     if st.get("walk_ms_list"):
         wl = st["walk_ms_list"]
         h = len(wl) // 3
