@@ -989,29 +989,6 @@ __global__ __launch_bounds__(128) void k_tile_topk(
   }
 }
 
-// fp32 score of one (user, item) pair: the chain of lg_score_topk_f32 / the MFMA tile,
-//   acc = 0; for s < D/4: for g < 4: acc = fmaf(u[g*D/4+s], i[g*D/4+s], acc),
-// with u in LDS (read as a broadcast) and the item row from global memory.
-template <int D>
-__device__ __forceinline__ float chain_score(const float *us, const float *__restrict__ it) {
-  constexpr int Q = D / 4;
-  float a = 0.f;
-#pragma unroll 1
-  for (int s0 = 0; s0 < Q; s0 += 4) {
-    float4 q[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) q[g] = *reinterpret_cast<const float4 *>(it + g * Q + s0);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float x = s == 0 ? q[g].x : (s == 1 ? q[g].y : (s == 2 ? q[g].z : q[g].w));
-        a = fmaf(us[g * Q + s0 + s], x, a);
-      }
-  }
-  return a;
-}
-
 // ------------------------------------------------------------ the tile walk kernel
 // One launch per tile. Persistent waves (NW per workgroup, one workgroup per CU; each wave
 // takes users u, u + G, u + 2G, ... with G = all waves). A wave's work is a stream of
@@ -1072,13 +1049,11 @@ struct WalkArgs {
 // accumulator columns per wave: the tile rounded up to whole 512-column scan steps
 __host__ __device__ constexpr int acc_cols(int tile) { return (tile + 511) / 512 * 512; }
 
-// per wave: acc[acc_cols(tile)], the overflow list (decode) and the user's embedding (MODE_TOPK with
-// D > 0; the running list itself lives in registers)
+// per wave: acc[acc_cols(tile)] and the overflow list (decode; the exact-score queue during
+// the scan); the running list itself lives in registers
 template <int MODE, int D, int M>
 __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
-  return ((size_t)acc_cols(tile) * 8 + (size_t)kOvfList * 12 +
-          (MODE == MODE_TOPK && D > 0 ? (size_t)D * 4 : 0) + 15) &
-         ~(size_t)15;
+  return ((size_t)acc_cols(tile) * 8 + (size_t)kOvfList * 12 + 15) & ~(size_t)15;
 }
 __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
   // class table + the block's rb maxima + rb of the tile's columns
@@ -1176,8 +1151,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   const uint32_t dummy_addr = acc_base + 8u * (uint32_t)(acc_cols(tile) + lane);
   double *ovl_ra = acc + acc_cols(tile);  // overflow list (decode)
   uint32_t *ovl_ent = reinterpret_cast<uint32_t *>(ovl_ra + kOvfList);
-  float *us = reinterpret_cast<float *>(ovl_ent + kOvfList);  // the user's row (D > 0)
-  (void)us;
 
   for (int c = threadIdx.x; c < kInvTab; c += blockDim.x) s_inv[c] = a.g_inv[c];
   double rmax = 0.0;  // the tile's largest rb (top-K prefilter)
@@ -1435,7 +1408,6 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         if (lane >= k) { L0 = neg_inf<double>(); I0 = kPadId; }
         kth(tau, tau_id);
       };
-      bool us_ready = false;  // the user's embedding row is copied to LDS at the first score
       // excluded items of this tile (the next run of the user's sorted exclusion row): -1
       const int32_t lim = a.item_begin + a.width;
       if (a.ex_rowptr) {
@@ -1456,19 +1428,47 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       // fl(gb fl(acc rb_j)) > tau is covered by the 2^-50 margin); those get rb_j and (with G)
       // the exact score. The list order (value desc, id asc) is total, so the order in which
       // candidates are inserted does not matter.
-      // the user's embedding row, copied to LDS before its first exact score (D > 0)
-      auto need_us = [&]() __attribute__((always_inline)) {
+      // Exact scores in batches (D > 0): the columns that pass the bound test are queued in
+      // LDS (column, f) and scored 16 at a time by v_mfma_f32_16x16x4_f32 -- candidate m as
+      // A row m (its item row), the user row as every B column -- whose per-element sums are
+      // the fp32 chain acc = fmaf(u[g*D/4+s], i[g*D/4+s], acc) (s outer, g inner) of
+      // lg_score_topk_f32. One load round trip per 16 candidates instead of a dependent
+      // per-lane chain of item-row loads; the queue is flushed when it holds 16, when the list
+      // is not full yet (tau = -inf: every column passes), and at the end of the scan.
+      int ncand = 0;
+      double *cq_f = ovl_ra;     // queued f (the decode's overflow list, free during the scan)
+      uint32_t *cq_j = ovl_ent;  // queued column
+      auto flush = [&]() __attribute__((always_inline)) {
         if constexpr (D > 0) {
-          if (!us_ready) {
-            const float e0 = a.eu[u * D + (lane < D ? lane : 0)];
-            if (lane < D) us[lane] = e0;
-            if constexpr (D > 64) {
-              const float e1 = a.eu[u * D + (64 + lane < D ? 64 + lane : 0)];
-              if (64 + lane < D) us[64 + lane] = e1;
+          constexpr int Qd = D / 4;              // MFMA steps
+          constexpr int H = Qd < 16 ? Qd : 16;   // steps per load round (<= 16 VGPRs each)
+          wave_sync();
+          const int m = lane & 15, g = lane >> 4;
+          for (int b0 = 0; b0 < ncand; b0 += 16) {
+            const int nb = ncand - b0 < 16 ? ncand - b0 : 16;
+            const int ci = b0 + (m < nb ? m : 0);
+            const float *ir = a.ei + (int64_t)(a.item_begin + (int)cq_j[ci]) * D + g * Qd;
+            const float *ur = a.eu + u * D + g * Qd;
+            f32x4 sc4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int h0 = 0; h0 < Qd; h0 += H) {
+              float av[H], bv[H];
+              load_frag<H>(ir + h0, av);
+              load_frag<H>(ur + h0, bv);
+#pragma unroll
+              for (int s = 0; s < H; ++s)
+                sc4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], sc4, 0, 0, 0);
             }
-            us_ready = true;
-            wave_sync();
+            // candidate mm's sum: lane 16 (mm / 4), element mm % 4
+            for (int mm = 0; mm < nb; ++mm) {
+              const float e = (mm & 3) == 0 ? sc4[0] : (mm & 3) == 1 ? sc4[1]
+                            : (mm & 3) == 2 ? sc4[2] : sc4[3];
+              const float sc = __shfl(e, 16 * (mm >> 2));
+              insert1((double)sc * cq_f[b0 + mm], a.item_begin + (int)cq_j[b0 + mm]);
+            }
           }
+          ncand = 0;
+          wave_sync();
         }
       };
       // The scan, 512 columns per iteration: lane l takes columns c0 + 4l .. + 3 and
@@ -1553,19 +1553,17 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
                               __shfl(bq_v, (j >> 6) & 63);
             const bool cand = has && bq * f > tau;
-            if (__ballot(cand)) {
-              need_us();
-              double v = 0.0;
-              const int item = a.item_begin + j;
+            const uint64_t bal = __ballot(cand);
+            if (bal) {
+              const int nb = __popcll(bal);
+              if (ncand + nb > kOvfList) flush();
               if (cand) {
-                v = (double)chain_score<D>(us, a.ei + (int64_t)item * D) * f;
+                const int p = ncand + __popcll(bal & lanemask_lt());
+                cq_f[p] = f;
+                cq_j[p] = (uint32_t)j;
               }
-              uint64_t bal = __ballot(cand && before(v, item, tau, tau_id));
-              while (bal) {
-                const int l = __ffsll((long long)bal) - 1;
-                bal &= bal - 1;
-                insert1(__shfl(v, l), __shfl(item, l));
-              }
+              ncand += nb;
+              if (ncand >= 16 || tau == neg_inf<double>()) flush();
             }
           } else {
             uint64_t bal = __ballot(has && before(f, a.item_begin + j, tau, tau_id));
@@ -1578,6 +1576,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           }
         }
       }
+      if (ncand) flush();
       if (dirty) {
         if (lane < k) {
           a.io_val[u * k + lane] = I0 != kPadId ? L0 : neg_inf<double>();
