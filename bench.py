@@ -48,6 +48,10 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 F32_MFMA_PEAK_TF = 157.3    # dense fp32 MFMA (= fp32 vector) peak, same table
+# chip-wide ds_add_f64 rate to random columns of a per-wave 2048-entry accumulator, 8 waves
+# per CU (scripts/micro/lds_atomic.hip on the box, profiles/r03_lds_atomic.txt): the ceiling
+# of the K3s walk, which adds every 3-hop path with one LDS atomic
+LDS_F64_ADD_PEAK_G = 1584.4
 
 WORKLOADS = {
     # name: (users, items, interactions, dim, layers)
@@ -409,17 +413,45 @@ def bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev, n_test=10_000_00
             "path": "lg_rec_hits + lg_rec_pair_overlap + lg_rec_intra_similarity_f64"}
 
 
-def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
+def spread_parity_field(idx, u0, u1, A, eu, ei, lam, k, n=256, top=16, seed=11):
+    """spread.parity_vs_oracle: ``n`` users of this rank's block (its `top` highest-degree
+    users, the first and last, the rest at random) against the oracle's fp64 path-order
+    restatement of S = G * F (oracle.spread_parity; the checker, run after the timed region
+    on the host cores): identical / tie-affected / mismatched counts."""
+    import numpy as np
+    from oracle import lgcn_oracle as O  # noqa: F401  (the checker)
+    nb = u1 - u0
+    deg = A.by_user.degrees()[u0:u1].cpu().numpy()
+    fixed = np.unique(np.concatenate([np.argsort(-deg, kind="stable")[:top], [0, nb - 1]]))
+    rest = np.random.default_rng(seed).choice(np.setdiff1d(np.arange(nb), fixed),
+                                              max(0, min(n, nb) - fixed.size), replace=False)
+    rows = np.sort(np.concatenate([fixed, rest]))
+    got = idx[torch.as_tensor(rows, device=idx.device)].cpu().numpy()
+    t0 = time.perf_counter()
+    r = O.spread_parity(got, rows + u0, A.by_user.rowptr.cpu().numpy(),
+                        A.by_user.col.cpu().numpy(), A.by_item.rowptr.cpu().numpy(),
+                        A.by_item.col.cpu().numpy(), A.n_items, lam, eu.cpu().numpy(),
+                        ei.cpu().numpy(), k)
+    r["seconds_cpu"] = time.perf_counter() - t0
+    r["rule"] = ("sets equal, or every differing item's exact fp64 S = G*F within both "
+                 "methods' rounding bounds (fp32 dot for G, 1e-12 rel for F) of the "
+                 "oracle's k-th exact S; users: the 16 highest-degree, first, last, random")
+    return r
+
+
+def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, extras=True,
+                 parity=True):
     """C5 LGCNHS recommendation for EVERY user (SpreadLightGCN, model/SpreadLightGCN/model.py:
     107-153 + recommend.py:18-52): per user, top-k of G * F with F = A @ HybridS(A, general_W,
-    lam) and G the fp32 e0 score, train|val items dropped, over the factored tile path.
-    Sharded by item range (lgcnhs.dist.sharded_spread_topk): each rank builds only its own W
-    tiles and scores all users on them, then one all-to-all + merge gives each rank the final
-    lists of its user block. Timed end to end (max over ranks). Also the Douban-shaped dense
-    path (configs[2]: SpreadLightGCNOpti, lam=0.5) at N=1."""
+    lam) and G the fp32 e0 score (width = e0_orig's), train|val items dropped, over the
+    factored tile path. Sharded by item range (lgcnhs.dist.sharded_spread_topk): each rank
+    builds only its own W tiles and scores all users on them, then one all-to-all + merge
+    gives each rank the final lists of its user block. Timed end to end (max over ranks).
+    With ``extras`` also the evaluation of the lists and the Douban-shaped dense path
+    (configs[2]: SpreadLightGCNOpti, lam=0.5) at N=1; with ``parity`` (rank 0) the lists of
+    256 sampled users against the oracle (after the timed region)."""
     from lgcnhs import ops
     from lgcnhs.dist import item_range, sharded_spread_topk
-    from lgcnhs.synth import synth_interactions
     A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
     eu = e0_orig[:U].contiguous()
     ei = e0_orig[U:U + I].contiguous()
@@ -446,72 +478,146 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     filled = float((idx >= 0).float().mean().item())
-    # roofline of the walk kernel (lg_spread_tile_resource_topk_f64), this rank, per launch:
-    # algorithmic bytes = the W-row bytes it must gather (one 128-B line per (user, item) and
-    # tile + overflow units: stats w_bytes) + 12 B of item id / ra per (user, item) + the
-    # user's list read and written (2 k 16 B) + its score bounds (qstride + 4 nch B) + 16 B of
-    # row pointers; time = HIP events around each launch on its stream
+    # roofline of the walk kernel (lg_spread_tile_resource_topk_f64), this rank, per launch.
+    # Its binding resource is the LDS atomic unit (one ds_add_f64 per 3-hop path into the
+    # user's fp64 accumulator): achieved = the useful paths it adds per second (padding slots
+    # excluded), peak = the measured random-column ds_add_f64 rate. The HBM side is reported
+    # beside it: algorithmic bytes = the W-row bytes gathered (one 128-B line per (user, item)
+    # and tile + overflow units) + 12 B of item id / ra per (user, item) + the user's list
+    # read and written (2 k 16 B) + its score bounds (qstride + 4 nch B) + 16 B of row
+    # pointers; time = HIP events around each launch on its stream.
     walk = None
     if st.get("walk_launches"):
         nl = st["walk_launches"]
         per_user = 2 * k * 16 + st.get("qstride", 0) + 4 * st.get("nch", 0) + 16
         alg = (st["w_bytes"] + 12 * st["user_items"] + per_user * st["users"] * nl) / nl
         ms = st["t_walk_ms"] / nl
-        traffic, traffic_src = (None, {"status": "PMC record is for the 1M-item tile walk"})
-        if (U, I) == (1_000_000, 1_000_000) and tile == 2048:
+        traffic, traffic_src = (None, {"status": "PMC record is for the 1M-item d=64 walk"})
+        if (U, I) == (1_000_000, 1_000_000) and tile == 2048 and eu.shape[1] == 64:
             traffic, traffic_src = load_traffic("c5-d64", 1, "spread_tiled.hip",
                                                 "c5-d64/spread_walk")
-        walk = {"bound": "hbm", "achieved": alg / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg / ms / 1e6 / HBM_PEAK_GBS, "traffic": traffic,
-                "traffic_source": traffic_src,
+        gpaths = st["w_paths"] / nl / ms / 1e6
+        walk = {"bound": "lds-atomic", "achieved": gpaths, "peak": LDS_F64_ADD_PEAK_G,
+                "unit": "G path-adds/s", "frac": gpaths / LDS_F64_ADD_PEAK_G,
+                "peak_source": "profiles/r03_lds_atomic.txt (ds_add_f64, random columns, 8 "
+                               "waves per CU)",
                 "kernel": "lg_spread_tile_resource_topk_f64", "avg_launch_ms": ms,
-                "alg_bytes_per_launch": alg, "launches": nl,
-                "paths_per_launch": st["w_paths"] / nl,
+                "launches": nl, "paths_per_launch": st["w_paths"] / nl,
+                "hbm": {"achieved": alg / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": alg / ms / 1e6 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                        "traffic": traffic, "traffic_source": traffic_src},
                 "build_ms_per_tile": st["t_build_ms"] / nl,
-                "bounds_ms_per_tile": st["t_bounds_ms"] / nl,
-                "note": "latency / LDS-atomic bound (one ds_add_f64 per path); bytes are "
-                        "the W lines gathered, not a bandwidth limit"}
-    evaluation = None
-    try:
-        evaluation = bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev)
-    except Exception as ex:  # a side measurement never hides the main result
-        log(f"eval bench failed: {ex!r}")
-    del A, idx
-    torch.cuda.empty_cache()
-    res = {"recs_per_s": U / dt, "users": U, "seconds": dt, "k": k, "lambda": lam,
-           "paths_per_s": paths / dt,
-           "row_bytes_GBps": nbytes / dt / 1e9,
+                "bounds_ms_per_tile": st["t_bounds_ms"] / nl}
+    res = {"recs_per_s": U / dt, "users": U, "dim": int(eu.shape[1]), "seconds": dt, "k": k,
+           "lambda": lam, "paths_per_s": paths / dt, "row_bytes_GBps": nbytes / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled, "roofline": walk,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_group_{cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
-                   "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64",
-           "eval": evaluation}
-    if world == 1:
-        # configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), dense
-        # general_W / W (fp64 I x I), fused G * F top-k
-        du, di, de = 600, 20_000, 60_000
-        users, items = synth_interactions(du, di, de, seed=3, dist="zipf")
-        g = torch.Generator(device=dev).manual_seed(42)
-        deu = torch.randn(du, 64, device=dev, generator=g) * 0.1
-        dei = torch.randn(di, 64, device=dev, generator=g) * 0.1
-
-        def dense():
-            Ad = ops.Interactions.from_pairs(torch.as_tensor(users), torch.as_tensor(items), du,
-                                             di, dev)
-            W = ops.hybrid_weight(ops.spread_general(Ad), Ad.k_item, lam)
-            return ops.spread_topk(Ad, W, k, Ad.by_user, True, deu, dei)
-        dense()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dense()
-        torch.cuda.synchronize()
-        dd = time.perf_counter() - t0
-        res["c3_douban_shape"] = {"users": du, "items": di, "interactions": de, "seconds": dd,
-                                  "recs_per_s": du / dd,
-                                  "path": "lg_spread_general_f64 + lg_hybrid_weight_f64 + "
-                                          "lg_spread_resource_f64 + lg_rows_topk_f64"}
+                   "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64"}
+    if parity and rank == 0:
+        try:
+            res["parity_vs_oracle"] = spread_parity_field(idx, u0, u1, A, eu, ei, lam, k)
+        except Exception as ex:  # the checker never hides the measured result
+            log(f"spread parity failed: {ex!r}")
+    if extras:
+        try:
+            res["eval"] = bench_eval(idx, u0, u1, A, keys, U, I, k, rank, world, dev)
+        except Exception as ex:  # a side measurement never hides the main result
+            log(f"eval bench failed: {ex!r}")
+    del A, idx
+    torch.cuda.empty_cache()
+    if extras and world == 1:
+        res["c3_douban_shape"] = bench_dense_spread(dev, k, lam)
         torch.cuda.empty_cache()
     return res
+
+
+def bench_dense_spread(dev, k, lam):
+    """configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), the
+    dense spreading path (general_W and W as fp64 I x I matrices, fused G * F top-k), end to
+    end and per kernel with HIP events, each against its roofline (algorithmic bytes / HBM
+    peak; general_W: the I x I write, hybrid: read + write, resource: the W rows gathered per
+    (user, item) + the F write, rows top-k: the F read)."""
+    from lgcnhs import ops
+    from lgcnhs.synth import synth_interactions
+    du, di, de = 600, 20_000, 60_000
+    users, items = synth_interactions(du, di, de, seed=3, dist="zipf")
+    g = torch.Generator(device=dev).manual_seed(42)
+    deu = torch.randn(du, 64, device=dev, generator=g) * 0.1
+    dei = torch.randn(di, 64, device=dev, generator=g) * 0.1
+
+    def dense(ev=None):
+        mark = (lambda i: ev[i].record()) if ev else (lambda i: None)
+        mark(0)
+        Ad = ops.Interactions.from_pairs(torch.as_tensor(users), torch.as_tensor(items), du,
+                                         di, dev)
+        mark(1)
+        gW = ops.spread_general(Ad)
+        mark(2)
+        W = ops.hybrid_weight(gW, Ad.k_item, lam)
+        del gW
+        mark(3)
+        F = ops.spread_resource(Ad, W)
+        mark(4)
+        out = ops.rows_topk(F, k, Ad.by_user, True, deu, dei)
+        mark(5)
+        return out
+    dense()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    t0 = time.perf_counter()
+    dense(ev)
+    torch.cuda.synchronize()
+    dd = time.perf_counter() - t0
+    ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(5)]
+    I2 = 8.0 * di * di
+    kern = {
+        "lg_spread_general_f64": (ms[1], I2),
+        "lg_hybrid_weight_f64": (ms[2], 2 * I2),
+        "lg_spread_resource_f64": (ms[3], 8.0 * de * di + 8.0 * du * di),
+        "lg_rows_topk_f64": (ms[4], 8.0 * du * di),
+    }
+    roof = {n: {"ms": t, "alg_bytes": b, "achieved_GBs": b / t / 1e6,
+                "frac": b / t / 1e6 / HBM_PEAK_GBS} for n, (t, b) in kern.items()}
+    return {"users": du, "items": di, "interactions": de, "seconds": dd, "recs_per_s": du / dd,
+            "kernels": roof, "setup_ms": ms[0],
+            "path": "lg_spread_general_f64 + lg_hybrid_weight_f64 + lg_spread_resource_f64 + "
+                    "lg_rows_topk_f64"}
+
+
+def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
+    """Masked full-catalog top-k (lg_score_topk_f32) for a block of ``nu`` users per rank
+    over all items: recs/s over ranks, MFMA fraction. Returns (line, GPU lists of users
+    [0, nu) when this rank's block starts at user 0, else None)."""
+    from lgcnhs import ops
+    from lgcnhs.graph import RowSets
+    nu = min(nu, U)
+    u0 = (rank * nu) % max(1, U - nu + 1)
+    eu = e0_orig[u0:u0 + nu].contiguous()
+    ei = e0_orig[U:U + I].contiguous()
+    ku = keys[(keys >= u0 * I) & (keys < (u0 + nu) * I)]  # this block's positives
+    excl = RowSets.from_pairs(ku // I - u0, ku % I, nu, I, dev)
+    ops.score_topk(eu, ei, k, excl)  # warm-up
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    reps = 3
+    for _ in range(reps):
+        ops.score_topk(eu, ei, k, excl)
+    e.record()
+    torch.cuda.synchronize()
+    tk = s.elapsed_time(e) / 1e3 / reps
+    if world > 1:
+        t = torch.tensor([tk], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tk = float(t.item())
+    flops = 2.0 * nu * I * D
+    line = {"recs_per_s": nu * world / tk, "users_per_rank": nu, "items": I, "k": k, "dim": D,
+            "ms": tk * 1e3, "tflops_per_gpu": flops / tk / 1e12,
+            "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
+            "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
+    lists = ops.score_topk(eu, ei, k, excl)[1] if u0 == 0 else None
+    return line, lists
 
 
 def load_traffic(workload, world, src_name="spmm.hip", key=None):
@@ -604,7 +710,9 @@ def main():
     ap.add_argument("--no-small", action="store_true",
                     help="skip the ML-1M-shaped (configs[1]) side measurement at N=1")
     ap.add_argument("--extra-dims", type=int, nargs="*", default=[128],
-                    help="also time the same graph at these embedding widths")
+                    help="also time the same graph's propagation at these embedding widths")
+    ap.add_argument("--extra-dim-legs", type=int, nargs="*", default=[128],
+                    help="... and its top-K and spread legs at these widths (C5: d=128)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="sub-chunks per rank per layer (per half with --layout bipartite) "
                          "for comm/compute overlap (0 = auto)")
@@ -690,7 +798,8 @@ def main():
     job_bytes = nnz * (8 + 4 * D) + N * (4 + 4 * D)  # one layer of the whole graph
     traffic, traffic_src = load_traffic(args.workload, world)
 
-    # the same graph at the other embedding widths the configs name (C5: d=128)
+    # the same graph at the other embedding widths the configs name (C5: d=128): the
+    # propagation, and (--extra-dim-legs) the e0 top-K and the LGCNHS spread leg at that width
     extra = {}
     for d2 in args.extra_dims:
         if d2 == D:
@@ -703,6 +812,22 @@ def main():
                            "unit": "edge-layers/s", "ms_per_step": el2 / max(2, args.steps // 2) * 1e3,
                            "roofline_frac": b2 / k2 / 1e9 / HBM_PEAK_GBS,
                            "achieved_GBs": b2 / k2 / 1e9}
+        if d2 in args.extra_dim_legs:
+            e2o = e2  # original node order (time_propagation permutes its own copy)
+            if not args.no_topk:
+                try:
+                    extra[f"d{d2}"]["topk"], _ = bench_topk(e2o, keys, U, I, d2, args.k,
+                                                            args.topk_users, rank, world, dev)
+                except Exception as ex:
+                    log(f"d{d2} topk bench failed: {ex!r}")
+            if not args.no_spread:
+                try:
+                    extra[f"d{d2}"]["spread"] = bench_spread(
+                        keys, U, I, e2o, args.k, rank, world, dev, extras=False,
+                        parity=not args.no_cpu_baseline)
+                except Exception as ex:
+                    log(f"d{d2} spread bench failed: {ex!r}")
+            del e2o
         del e2
         torch.cuda.empty_cache()
 
@@ -717,37 +842,14 @@ def main():
 
     topk = topk_gpu_lists = None
     if not args.no_topk:
-        nu = min(args.topk_users, U)
-        u0 = (rank * nu) % max(1, U - nu + 1)
-        eu = e0_orig[u0:u0 + nu].contiguous()
-        ei = e0_orig[U:U + I].contiguous()
-        ku = keys[(keys >= u0 * I) & (keys < (u0 + nu) * I)]  # this block's positives
-        excl = RowSets.from_pairs(ku // I - u0, ku % I, nu, I, dev)
-        ops.score_topk(eu, ei, args.k, excl)  # warm-up
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        reps = 3
-        for _ in range(reps):
-            ops.score_topk(eu, ei, args.k, excl)
-        e.record()
-        torch.cuda.synchronize()
-        tk = s.elapsed_time(e) / 1e3 / reps
-        if world > 1:
-            t = torch.tensor([tk], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tk = float(t.item())
-        flops = 2.0 * nu * I * D
-        topk = {"recs_per_s": nu * world / tk, "users_per_rank": nu, "items": I, "k": args.k,
-                "ms": tk * 1e3, "tflops_per_gpu": flops / tk / 1e12,
-                "mfma_frac": flops / tk / 1e12 / F32_MFMA_PEAK_TF,
-                "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}
-        topk_gpu_lists = ops.score_topk(eu, ei, args.k, excl)[1] if u0 == 0 else None
+        topk, topk_gpu_lists = bench_topk(e0_orig, keys, U, I, D, args.k, args.topk_users,
+                                          rank, world, dev)
 
     spread = None
     if not args.no_spread:
         try:
-            spread = bench_spread(keys, U, I, e0_orig, args.k, rank, world, dev)
+            spread = bench_spread(keys, U, I, e0_orig, args.k, rank, world, dev,
+                                  parity=not args.no_cpu_baseline)
         except Exception as ex:  # a side measurement never hides the main result
             log(f"spread bench failed: {ex!r}")
 

@@ -90,7 +90,9 @@ def main() -> dict:
     name, k = cfg.MODEL["name"], cfg.RECOMMEND["k"]
     path = cfg.RECOMMEND["save_path"] + "all_user_recommend_dict_" + name + str(k) + ".npy"
     try:
-        # a dict this package's recommenders saved (lgcnhs.recs.save_recs), as the reference does
+        # a dict this package's recommenders saved (lgcnhs.recs.save_recs), as the reference
+        # does; the name has no "_" before k, as in reference main.py:62, so (as there) only
+        # LightGCNOpti's saver (no "_" either) hits this cache and the others recompute
         all_user_recommend_dict = np.load(path, allow_pickle=True).item()
         logger.info("推荐结果读取完毕")
     except FileNotFoundError:

@@ -96,6 +96,10 @@ def test_gpu_spread_opti_douban_matches_reference(golden, monkeypatch, tmp_path)
     # or G*F = -0.0), ordered arbitrarily by the reference's argsort: allowed, but their
     # positive-score prefix must match
     ties = compare_topk_sets(got, g["recs"], gaps, tol=1e-12 * np.nanmax(np.abs(gaps)),
-                             max_tie_frac=0.1, got_vals=vals.cpu().numpy())
+                             max_tie_frac=1.0, got_vals=vals.cpu().numpy())
+    exact_ties = int((gaps[:, 0] == gaps[:, 1]).sum())
     print(f"[C3 SpreadLightGCNOpti douban-shape] tie-affected users: {ties} of {U} "
-          f"(exact 0.0 ties at the K boundary: {int((gaps[:, 0] == gaps[:, 1]).sum())})")
+          f"(exact 0.0 ties at the K boundary: {exact_ties})")
+    # the exact-tie users (equal k-th / (k+1)-th reference values: any order is the
+    # reference's) plus at most 1 % rounding-level ties
+    assert ties <= exact_ties + max(1, U // 100)

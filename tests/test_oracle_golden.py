@@ -156,3 +156,45 @@ def test_spread_rows_sparse_equals_dense_restatement(golden, lam):
     users = np.array([0, 5, 17, U - 1])
     Fs = O.spread_rows_sparse(urp, ii, irp, uu[order], I, users, lam)
     np.testing.assert_allclose(Fs, F[users], rtol=1e-12, atol=1e-15 * np.abs(F).max())
+
+
+@pytest.mark.parametrize("name", ["spread_toy", "spread_edge"])
+def test_spread_row_paths_equals_reference_F(golden, name):
+    """The path-order restatement behind the C5 LGCNHS parity (spread_row_paths) against
+    the reference's own F matrices (the fixtures' F_j, every lambda of the file)."""
+    g = golden(name)
+    U, I, A = _spread_case(g)
+    uu, ii = np.nonzero(A)
+    urp = np.searchsorted(uu, np.arange(U + 1))
+    order = np.lexsort((uu, ii))
+    irp = np.searchsorted(ii[order], np.arange(I + 1))
+    for j, lam in enumerate(g["lambdas"]):
+        F = np.stack([O.spread_row_paths(urp, ii, irp, uu[order], I, u, float(lam))
+                      for u in range(U)])
+        np.testing.assert_allclose(F, g[f"F_{j}"], rtol=1e-12,
+                                   atol=1e-15 * np.abs(g[f"F_{j}"]).max())
+
+
+def test_spread_parity_counts_reference_lists(golden):
+    """spread_parity on lists taken from the dense restatement (G * F, interactions
+    dropped): every user identical; a corrupted list is counted as mismatched."""
+    g = golden("spread_ml100k")
+    U, I, A = _spread_case(g)
+    F = O.get_resource(A, O.hybrid_s(A, O.spreading_general_mat(A.copy()), 0.5))
+    rng = np.random.default_rng(3)
+    eu = (rng.normal(size=(U, 64)) * 0.1).astype(np.float32)
+    ei = (rng.normal(size=(I, 64)) * 0.1).astype(np.float32)
+    S = (eu.astype(np.float64) @ ei.astype(np.float64).T) * F
+    S[A != 0] = -np.inf
+    ref = np.argsort(-S, axis=1, kind="stable")[:, :10]
+    uu, ii = np.nonzero(A)
+    urp = np.searchsorted(uu, np.arange(U + 1))
+    order = np.lexsort((uu, ii))
+    irp = np.searchsorted(ii[order], np.arange(I + 1))
+    users = np.arange(0, U, 7)
+    r = O.spread_parity(ref[users], users, urp, ii, irp, uu[order], I, 0.5, eu, ei, 10)
+    assert r["identical"] == users.size and r["mismatched"] == 0
+    bad = ref[users].copy()
+    bad[0, 3] = int(np.argsort(S[users[0]])[I // 2])  # a mid-ranked item
+    assert O.spread_parity(bad, users, urp, ii, irp, uu[order], I, 0.5, eu, ei,
+                           10)["mismatched"] == 1
