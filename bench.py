@@ -461,8 +461,7 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, e
     t0 = time.perf_counter()
     st = {}  # paths added / row bytes gathered by the walk (the 3-hop paths of F = A W)
     (u0, u1), _, idx = sharded_spread_topk(A, lam, k, A.by_user, True, eu, ei, rank=rank,
-                                           world=world, tile=tile, scratch_bytes=32 << 30,
-                                           stats=st)
+                                           world=world, tile=tile, stats=st)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     # the walk's paths / row bytes: counted from the tiles after the timed run (untimed)

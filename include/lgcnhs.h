@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 7
+#define LG_ABI_VERSION 8
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -208,18 +208,15 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
  * holding an I x I or U x I matrix, as
  *   F[u][j] = rb_j * sum over the paths u -> i -> v -> j of fl(1/k_v) * ra_i
  * (ra = 1/alpha, rb = 1/beta; each term within a few ulp of the reference's W entry, the
- * summation order the walk's own, fixed). For each tile [j0, j0 + tile) of item columns the
- * caller runs: lg_spread_tile_cursor -> lg_spread_tile_bound -> (exclusive prefix of the
- * rows' overflow units = ovf_ptr) -> lg_spread_tile_rows_f64 -> lg_spread_tile_resource_f64
- * (F) or lg_spread_tile_resource_topk_f64 (running top-K lists). The orchestration
- * (lgcnhs.ops.spread_topk_tiled) is host code; see DESIGN.md §5 K3s.
+ * summation order the walk's own, fixed). Tiles [j0, j0 + tile) of item columns are built
+ * a group of <= 8 at a time: lg_spread_group_cursor -> lg_spread_group_bound ->
+ * lg_spread_group_units -> (inclusive scan of the units) -> lg_spread_group_rows_f64; each
+ * tile is then walked by lg_spread_tile_resource_topk_f64 (running top-K lists), with
+ * lg_score_chunk_bound's score bounds when there is a G factor. The orchestration
+ * (lgcnhs.ops.spread_topk_tiled) is host code; see DESIGN.md §5 K3s. The per-tile build
+ * passes, the F-writing walk and the two-kernel top-K merge that these replace are kept,
+ * as bitwise references for the tests, in include/lgcnhs_ref.h (lib/liblgcnhs_ref.so only).
  * ------------------------------------------------------------------------------------ */
-
-/* alpha[i] = k_item[i]^(1 - lambda), beta[i] = k_item[i]^lambda: the HybridS degree
- * factors (model/SpreadMethod/model.py:74-79), computed with the same pow() as
- * lg_hybrid_weight_f64. */
-int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
-                          double *alpha, double *beta, lg_stream_t stream);
 
 /* ra[i] = 1 / alpha[i], rb[i] = 1 / beta[i] (a zero factor -> 1: the reference's den == 0
  * rule, model/SpreadMethod/model.py:81-82; such rows / columns hold no paths). */
@@ -231,52 +228,20 @@ int lg_hybrid_recip_f64(const double *k_item, int64_t n_items, double lambda, do
 int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *inv,
                       lg_stream_t stream);
 
-/* end[v] = first position p >= cur[v] of user v's item row (user_rowptr/user_items, items
- * ascending) with user_items[p] >= item_end (or the row end), count[v] = end[v] - cur[v].
- * With cur = the row starts (first tile) or the previous tile's end,
- * user_items[cur[v] .. end[v]) are v's items in the tile. cur and end must not alias;
- * item_end - (the tile's first item) <= 8192 (count is 16-bit). */
-int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
-                          int64_t n_users, int32_t item_end, const int64_t *cur,
-                          int64_t *end, uint16_t *count, lg_stream_t stream);
-
-/* bound[i] = sum over users v of item i (item_rowptr/item_users) of count[v]: the number of
- * (user, tile item) pairs behind W's row i in the tile (its paths). */
-int lg_spread_tile_bound(const int64_t *item_rowptr, const int32_t *item_users,
-                         int64_t n_items, const uint16_t *count, int64_t *bound,
-                         lg_stream_t stream);
-
-/* Row i of general_W restricted to the tile, for every item i, as one 128-byte line at
- * lines + 128 i (32 uint32 words) plus, for rows that do not fit, a run of 16-byte units in
- * ovf. Word 0 = header: bit 31 V format, bit 30 overflow, bits 0-28 the run's first unit
- * (whose .x = the number of data units after it).
+/* Line format of a tile (lgcnhs_ref.h lg_spread_tile_rows_f64 builds one tile at a time):
+ * row i of general_W restricted to the tile as one 128-byte line at lines + 128 i (32
+ * uint32 words) plus, for rows that do not fit, a run of 16-byte units in ovf. Word 0 =
+ * header: bit 31 V format, bit 30 overflow, bit 29 "slow" (V rows, P rows with a class
+ * >= 512), bits 0-28 the run's first unit (whose .x = the number of data units after it).
  *   P rows (bound[i] <= vthr): one word per (user v, item j) pair behind the row, users
  *     ascending then items ascending: bits 0-15 j - item_begin, bits 16-30 user_cls[v] (a
- *     1-based class of v's degree, < 0x8000: inv_cls[user_cls[v]] = fl(1/k_v)); 0 =
- *     padding; bit 31 clear. Line words 1-31 then 4 per data unit.
+ *     1-based class of v's degree: inv_cls[user_cls[v]] = fl(1/k_v)); 0 = padding.
  *   V rows (hub items, bound[i] > vthr): one 16-byte entry per distinct column, ascending:
- *     {0x80000000 | (j - item_begin), fp64 general_W[i][j] (lo, hi), 0}. Line units 1-7 then
- *     1 per data unit.
- * ovf_ptr[i] = the caller's exclusive prefix over rows of their overflow units:
- * 1 + ceil((bound - 31) / 4) for P rows with bound > 31, 1 + (min(bound, tile) - 7) for V
- * rows with min(bound, tile) > 7, else 0; ovf must hold that total + 64 units (the walk
- * reads 64 units per run). row_len[i] (optional) = the row's pairs (P) or entries (V).
- * Header bit 29 ("slow") marks V rows and P rows with a class >= 512 (the walk's general
- * decode); the overflow pointer has 29 bits. Lambda-independent (a sweep reuses the tile).
- * Line n_items (the walk's padding row) is never written: the caller zeroes it. cur/count from lg_spread_tile_cursor, bound
- * from lg_spread_tile_bound, inv_deg from lg_inv_degree_f64 over the user rows (V rows).
- * ws: lg_spread_tile_rows_ws_bytes(n_items) bytes of scratch. tile in [1, 8192];
- * vthr >= 31; every item of the tile lies in [item_begin, item_begin + tile). */
-size_t lg_spread_tile_rows_ws_bytes(int64_t n_items);
-int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_users,
-                            const int32_t *user_items, const uint16_t *user_cls,
-                            const double *inv_deg, int64_t n_items, const int64_t *cur,
-                            const uint16_t *count, int32_t item_begin, int32_t tile,
-                            const int64_t *bound, int64_t vthr, const int64_t *ovf_ptr,
-                            void *lines, void *ovf, int32_t *row_len, void *ws,
-                            size_t ws_bytes, lg_stream_t stream);
-
-/* Group build: the three calls above for n_tiles (<= 8) consecutive tiles at once, each
+ *     {0x80000000 | (j - item_begin), fp64 general_W[i][j] (lo, hi), 0}.
+ * Lambda-independent (a sweep reuses the tile); line n_items (the walk's padding row) is
+ * zeroed by the caller.
+ *
+ * Group build: n_tiles (<= 8) consecutive tiles at once, each
  * (item row, user) pair visited once per group instead of once per tile. Tile t of the group
  * is [group_begin + t tile, min(group_begin + (t + 1) tile, stop)).
  * lg_spread_group_cursor: counts[v][0..7] (8 uint16 per user, 16-byte aligned, unused
@@ -284,14 +249,14 @@ int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t *item_user
  *   (cur[v] = the first position with item >= group_begin; cur and end must not alias;
  *   positions < 2^32), rec[v] (16 bytes per user, 16-byte aligned) = the user's record for
  *   the rows pass: its class (user_cls) and up to 6 of its group items in place, else cur.
- * lg_spread_group_bound: bound[t][i] ([n_tiles][n_items] int64) = lg_spread_tile_bound of
- *   tile t.
+ * lg_spread_group_bound: bound[t][i] ([n_tiles][n_items] int64) = the (user, tile item)
+ *   pairs behind row i of W in tile t (its paths).
  * lg_spread_group_units: units[t][i] ([n_tiles][n_items] int64) = the overflow units of
  *   row i in tile t (1 + ceil((bound - 31) / 4) for P rows with bound > 31, 1 + (min(bound,
  *   width_t) - 7) for V rows with more than 7 entries, else 0); the caller's inclusive scan
  *   of the flat array (units_incl) places every run: tile t's runs start at unit
  *   units_incl[t n_items - 1] (0 for t = 0), each row's run at its exclusive prefix.
- * lg_spread_group_rows_f64: lg_spread_tile_rows_f64 of every tile t of the group, tile t's
+ * lg_spread_group_rows_f64: the lines and runs of every tile t of the group, tile t's
  *   lines at lines + t (n_items + 1) 128 bytes (each tile's line n_items zeroed by the
  *   caller), its runs in ovf as units_incl places them (header pointers relative to the
  *   tile's first unit: each tile's lines and runs are the per-tile build's, bit for bit);
@@ -317,32 +282,6 @@ int lg_spread_group_rows_f64(const int64_t *item_rowptr, const int32_t *item_use
                              const int64_t *units_incl, void *lines, void *ovf,
                              int32_t *row_len, void *ws, size_t ws_bytes, lg_stream_t stream);
 
-/* F[u][j - item_begin] = rb[j] * sum over the paths of u's items of the tile's rows (see the
- * section comment) for the n_users rows of user_rowptr (pass user_rowptr + u0 for a block)
- * and j in [item_begin, item_begin + tile) (columns >= item_begin + width are 0); F
- * row-major with leading dim ldf >= tile. ra_edge[p] = ra[user_items[p]] (aligned with
- * user_items, at least one entry), rbeta = rb of all items, inv_cls the class table;
- * lines / ovf from lg_spread_tile_rows_f64, with line null_row (= n_items: lines holds
- * n_items + 1) all zero. */
-int lg_spread_tile_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
-                                const double *ra_edge, int64_t n_users, const void *lines,
-                                const void *ovf, int32_t null_row, const double *rbeta,
-                                const double *inv_cls,
-                                int32_t item_begin, int32_t tile, int32_t width, double *F,
-                                int64_t ldf, lg_stream_t stream);
-
-/* Merge columns [item_begin, item_begin + n_cols) of (G *) F (F[r][0..n_cols), leading dim
- * ldf; G as in lg_rows_topk_f64 with eu = the rows' user embeddings and ei = all item
- * embeddings) into running top-K lists io_val/io_idx [n_rows][k] (sorted by value desc,
- * index asc; index -1 = empty). first != 0 ignores their contents. Exclusions as in
- * lg_rows_topk_f64 (ex_rowptr indexed by r). Applied over all tiles in ascending order the
- * lists equal lg_rows_topk_f64 over the full rows. k in [1, 128]. */
-int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int32_t item_begin,
-                     int32_t n_cols, const float *eu, const float *ei, int32_t dim,
-                     const int64_t *ex_rowptr, const int32_t *ex_col, int32_t excl_mode,
-                     int32_t k, int32_t first, double *io_val, int64_t *io_idx,
-                     lg_stream_t stream);
-
 /* cur[v] = first position of user v's item row (ascending) with item >= item_begin: the
  * cursor state for a tile walk that starts at item_begin (an item-range shard of a
  * multi-GPU run) instead of 0. */
@@ -351,25 +290,26 @@ int lg_spread_tile_seek(const int64_t *user_rowptr, const int32_t *user_items,
 
 /* Merge n_lists sorted top-K lists per row, in_val/in_idx laid out [n_lists][n_rows][k]
  * (value desc, index asc; index -1 = empty), into out_val/out_idx [n_rows][k] in the same
- * order: the per-item-range lists of lg_tile_topk_f64 (disjoint item ranges) give the lists
+ * order: the per-item-range lists of lg_spread_tile_resource_topk_f64 (disjoint item ranges,
+ * the multi-GPU shards) give the lists
  * a single walk over all items would. k in [1, 128]. */
 int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t n_lists,
                             int64_t n_rows, int32_t k, double *out_val, int64_t *out_idx,
                             lg_stream_t stream);
 
-/* Fused lg_spread_tile_resource_f64 + lg_tile_topk_f64 for one tile: each user's F columns
- * [item_begin, item_begin + width) are accumulated in LDS (the values lg_spread_tile_
- * resource_f64 writes, bit for bit) and merged straight into the running top-K lists
+/* The tile walk: each user's F columns [item_begin, item_begin + width) are accumulated in
+ * LDS (the values of the F-writing reference walk, lgcnhs_ref.h, bit for bit) and merged
+ * straight into the running top-K lists
  * io_val/io_idx [n_users][k] (first != 0: start empty); F is never written to memory. G
  * factor: eu = the rows' user embeddings, ei = all item embeddings, gb =
  * lg_score_chunk_bound's [n_users][n_chunks] bounds for this tile (n_chunks =
  * ceil(width / 64) <= 64) and optionally qb/qstride, its per-column 8-bit bounds: only
  * columns whose bound (gb * q / 255 with qb) times F can beat the K-th value get the exact
  * score chain.
- * Exclusions (dropped): ex_rowptr/ex_col as in lg_tile_topk_f64 plus a per-row cursor
+ * Exclusions (dropped): ex_rowptr/ex_col as in lg_rows_topk_f64 plus a per-row cursor
  * ex_cur[n_users] positioned at the walk's first item by lg_spread_tile_seek(ex_rowptr,
  * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
- * lg_tile_topk_f64 over lg_spread_tile_resource_f64's tiles. k in [1, 128]; dim in
+ * lg_rows_topk_f64 over the F rows the walk sums. k in [1, 128]; dim in
  * {32, 64, 128}. lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
  * workgroup's tables (the launch fits as many waves per CU as the LDS holds). */
 size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
@@ -401,10 +341,6 @@ int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_user
                          const void *i_bf16, const float *i_norm, int32_t dim,
                          int32_t item_begin, int32_t width, float *gb, uint8_t *qb,
                          int32_t qstride, lg_stream_t stream);
-
-/* out[r] = ||x[r]||_2 (fp64) for an fp32 [n_rows, dim] matrix. */
-int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,
-                     lg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Recommendation-list metrics (reference metrics/accurate.py and

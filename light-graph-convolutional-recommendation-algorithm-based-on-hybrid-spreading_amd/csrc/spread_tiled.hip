@@ -37,6 +37,17 @@
 
 #include "common.h"
 
+// LG_REFERENCE_PATHS (test-reference build, lib/liblgcnhs_ref.so, include/lgcnhs_ref.h): the
+// per-tile build passes, the F-writing walk and the two-kernel top-K merge, kept as bitwise
+// references for the product's group build and fused walk. The product library
+// (lib/liblgcnhs.so) is built without them.
+#ifndef LG_REFERENCE_PATHS
+#define LG_REFERENCE_PATHS 0
+#endif
+#if LG_REFERENCE_PATHS
+#include "lgcnhs_ref.h"
+#endif
+
 namespace lg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -72,30 +83,6 @@ constexpr int kLineSlots = 31;  // P slots in a line (word 0 is the header)
 constexpr int kLineEnts = 7;    // V entries in a line (unit 0 holds the header)
 constexpr int kInvTab = 512;    // degree classes whose fl(1/k) is cached in LDS
 
-__global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
-                                                        int64_t n, double lambda,
-                                                        double *__restrict__ alpha,
-                                                        double *__restrict__ beta) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  // the same pow() calls as k_hybrid_weight (spread.hip)
-  alpha[i] = pow(k_item[i], 1.0 - lambda);
-  beta[i] = pow(k_item[i], lambda);
-}
-
-// out[r] = ||x[r]||_2 in fp64 (the bound of the fused top-K prefilter).
-__global__ __launch_bounds__(256) void k_row_norms(const float *__restrict__ x, int64_t n,
-                                                   int dim, double *__restrict__ out) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  double s = 0.0;
-  for (int d = 0; d < dim; ++d) {
-    const double v = x[r * dim + d];
-    s += v * v;
-  }
-  out[r] = sqrt(s);
-}
-
 __global__ __launch_bounds__(256) void k_inv_degree(const int64_t *__restrict__ rowptr,
                                                     int64_t n, double *__restrict__ inv) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -103,6 +90,7 @@ __global__ __launch_bounds__(256) void k_inv_degree(const int64_t *__restrict__ 
   inv[v] = 1.0 / (double)(rowptr[v + 1] - rowptr[v]);  // k_spread_general's fl(1/k_v)
 }
 
+#if LG_REFERENCE_PATHS
 __global__ __launch_bounds__(256) void k_tile_cursor(const int64_t *__restrict__ user_rowptr,
                                                      const int32_t *__restrict__ user_items,
                                                      int64_t n_users, int32_t item_end,
@@ -119,6 +107,7 @@ __global__ __launch_bounds__(256) void k_tile_cursor(const int64_t *__restrict__
   count[v] = (uint16_t)(p - p0);  // <= tile <= 8192
 }
 
+#endif  // LG_REFERENCE_PATHS
 // cur[v] = first position of user v's item row with item >= item_begin: the cursor state
 // of a tile walk that starts at item_begin instead of 0 (an item-range shard).
 __global__ __launch_bounds__(256) void k_tile_seek(const int64_t *__restrict__ user_rowptr,
@@ -130,6 +119,7 @@ __global__ __launch_bounds__(256) void k_tile_seek(const int64_t *__restrict__ u
   cur[v] = lower_bound_i32(user_items, user_rowptr[v], user_rowptr[v + 1], item_begin);
 }
 
+#if LG_REFERENCE_PATHS
 // one wave per item row
 __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ item_rowptr,
                                                     const int32_t *__restrict__ item_users,
@@ -147,6 +137,7 @@ __global__ __launch_bounds__(256) void k_tile_bound(const int64_t *__restrict__ 
   if (lane == 0) bound[i] = s;
 }
 
+#endif  // LG_REFERENCE_PATHS
 // ra[i] = 1 / k_item[i]^(1 - lambda), rb[i] = 1 / k_item[i]^lambda (the same pow() calls as
 // k_hybrid_weight); a zero factor -> 1 (its rows / columns hold no paths).
 __global__ __launch_bounds__(256) void k_hybrid_recip(const double *__restrict__ k_item,
@@ -169,6 +160,7 @@ __device__ __forceinline__ void put_slot(uint32_t *__restrict__ line, uint32_t *
   else ovf[(ou + 1) * 4 + (p - kLineSlots)] = w;
 }
 
+#if LG_REFERENCE_PATHS
 // P rows: one wave per item row with bound[i] <= vthr pairs. Every word of the line and of
 // the overflow run is written exactly once (header, pairs, zero padding), so no stale data
 // of an earlier tile survives and no two stores of the wave hit one word.
@@ -293,6 +285,8 @@ __global__ __launch_bounds__(256) void k_tile_rows_hub(
     __syncthreads();
   }
 }
+
+#endif  // LG_REFERENCE_PATHS
 
 __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ bound,
                                                   int64_t n_items, int64_t vthr,
@@ -678,6 +672,7 @@ __device__ __forceinline__ void load_frag(const float *__restrict__ p, float (&v
   }
 }
 
+#if LG_REFERENCE_PATHS
 // Merge the tile's columns of (G *) F into running per-user top-K lists (io_val/io_idx,
 // sorted, index -1 = empty). D = 0: no G factor. One wave = NG groups of 16 users (rows);
 // lane (ul, gq) holds user ul of each group and items 4gq..4gq+3 of each 16-item step.
@@ -989,6 +984,8 @@ __global__ __launch_bounds__(128) void k_tile_topk(
   }
 }
 
+#endif  // LG_REFERENCE_PATHS
+
 // ------------------------------------------------------------ the tile walk kernel
 // One launch per tile. Persistent waves (NW per workgroup, one workgroup per CU; each wave
 // takes users u, u + G, u + 2G, ... with G = all waves). A wave's work is a stream of
@@ -1011,7 +1008,10 @@ __global__ __launch_bounds__(128) void k_tile_topk(
 constexpr int MODE_F = 0, MODE_TOPK = 1;
 constexpr int kWalkQ = 8;       // line loads per lane per batch: 8 rows each, 64 rows
 constexpr int kBatchRows = 8 * kWalkQ;
-constexpr int kOvfList = kBatchRows;
+// per-wave scratch list: the batch's overflow rows during the decode, the exact-score queue
+// (column, f) during the scan -- a drain round can queue one candidate per lane, so it holds
+// at least 64 entries whatever the batch size
+constexpr int kOvfList = kBatchRows > 64 ? kBatchRows : 64;
 constexpr int kDecodePhase = 4;  // lines whose class reads precede their adds
 // q dwords per lane loaded with the user's first batch (256 columns each), then streamed
 // kQPre / 2 scan iterations ahead (4 and 8 measured no faster than 2: 3.22 / 3.33 vs 3.20 s)
@@ -1556,7 +1556,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             const uint64_t bal = __ballot(cand);
             if (bal) {
               const int nb = __popcll(bal);
-              if (ncand + nb > kOvfList) flush();
+              if (ncand + nb > kOvfList) flush();  // (nb <= 64 <= kOvfList)
               if (cand) {
                 const int p = ncand + __popcll(bal & lanemask_lt());
                 cq_f[p] = f;
@@ -1625,6 +1625,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   }
 }
 
+#if LG_REFERENCE_PATHS
 template <int D, bool VEC>
 static void launch_tile_topk_v(int M, const double *F, int64_t ldf, int64_t n_rows, int32_t j0,
                                int32_t n_cols, const float *eu, const float *ei,
@@ -1676,6 +1677,8 @@ static void launch_tile_topk(int M, const double *F, int64_t ldf, int64_t n_rows
     launch_tile_topk_v<D, false>(M, F, ldf, n_rows, j0, n_cols, eu, ei, ex_rowptr, ex_col, drop, k,
                              first, io_val, io_idx, s);
 }
+
+#endif  // LG_REFERENCE_PATHS
 
 // Merge n_lists sorted top-K lists per row ([n_lists][n_rows][k], index -1 = empty) into one
 // ([n_rows][k]): the item-range shards of a multi-GPU spreading run. One wave per row, the
@@ -1765,15 +1768,6 @@ extern "C" int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_i
   return launch_status("lg_topk_lists_merge_f64");
 }
 
-extern "C" int lg_hybrid_factors_f64(const double *k_item, int64_t n_items, double lambda,
-                                     double *alpha, double *beta, lg_stream_t stream) {
-  LG_REQUIRE(k_item && alpha && beta && n_items >= 0, "lg_hybrid_factors_f64: bad arguments");
-  if (n_items == 0) return LG_OK;
-  k_hybrid_factors<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream>>>(k_item, n_items, lambda, alpha, beta);
-  return launch_status("lg_hybrid_factors_f64");
-}
-
 extern "C" int lg_hybrid_recip_f64(const double *k_item, int64_t n_items, double lambda,
                                    double *ra, double *rb, lg_stream_t stream) {
   LG_REQUIRE(k_item && ra && rb && n_items >= 0, "lg_hybrid_recip_f64: bad arguments");
@@ -1792,6 +1786,7 @@ extern "C" int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *
   return launch_status("lg_inv_degree_f64");
 }
 
+#if LG_REFERENCE_PATHS
 extern "C" int lg_spread_tile_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                                      int64_t n_users, int32_t item_end, const int64_t *cur,
                                      int64_t *end, uint16_t *count, lg_stream_t stream) {
@@ -1855,6 +1850,8 @@ extern "C" int lg_spread_tile_rows_f64(const int64_t *item_rowptr, const int32_t
       ovf_ptr, (uint32_t *)lines, (uint32_t *)ovf, row_len);
   return launch_status("lg_spread_tile_rows_f64");
 }
+
+#endif  // LG_REFERENCE_PATHS
 
 extern "C" int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t *user_items,
                                       const uint16_t *user_cls, int64_t n_users,
@@ -1981,6 +1978,7 @@ static int launch_walk(const WalkArgs &a, hipStream_t s) {
   return LG_OK;
 }
 
+#if LG_REFERENCE_PATHS
 extern "C" int lg_spread_tile_resource_f64(const int64_t *user_rowptr,
                                            const int32_t *user_items, const double *ra_edge,
                                            int64_t n_users, const void *lines, const void *ovf,
@@ -2046,6 +2044,8 @@ extern "C" int lg_tile_topk_f64(const double *F, int64_t ldf, int64_t n_rows,
   }
   return launch_status("lg_tile_topk_f64");
 }
+
+#endif  // LG_REFERENCE_PATHS
 
 extern "C" size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim) {
   // one wave's share plus the workgroup's tables (the launch fits as many waves as it can)
@@ -2131,11 +2131,3 @@ extern "C" int lg_spread_tile_resource_topk_f64(
   return launch_status("lg_spread_tile_resource_topk_f64");
 }
 
-extern "C" int lg_row_norms_f64(const float *x, int64_t n_rows, int32_t dim, double *out,
-                                lg_stream_t stream) {
-  LG_REQUIRE(x && out && n_rows >= 0 && dim >= 1, "lg_row_norms_f64: bad arguments");
-  if (n_rows == 0) return LG_OK;
-  k_row_norms<<<dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
-      x, n_rows, dim, out);
-  return launch_status("lg_row_norms_f64");
-}

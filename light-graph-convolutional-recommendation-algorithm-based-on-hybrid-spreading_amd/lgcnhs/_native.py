@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("LGCNHS_LIB_PATH") or LIB_PATH
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -70,17 +70,8 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp],
     ),
-    "lg_hybrid_factors_f64": (ctypes.c_int, [_vp, _i64, _f64, _vp, _vp, _vp]),
     "lg_hybrid_recip_f64": (ctypes.c_int, [_vp, _i64, _f64, _vp, _vp, _vp]),
     "lg_inv_degree_f64": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
-    "lg_spread_tile_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
-    "lg_spread_tile_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
-    "lg_spread_tile_rows_ws_bytes": (_sz, [_i64]),
-    "lg_spread_tile_rows_f64": (
-        ctypes.c_int,
-        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp,
-         _vp, _sz, _vp],
-    ),
     "lg_spread_group_cursor": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                                               _vp, _vp, _vp, _vp]),
     "lg_spread_group_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _vp, _vp]),
@@ -90,14 +81,6 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
          _vp, _vp, _vp, _sz, _vp],
-    ),
-    "lg_spread_tile_resource_f64": (
-        ctypes.c_int,
-        [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
-    ),
-    "lg_tile_topk_f64": (
-        ctypes.c_int,
-        [_vp, _i64, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
     ),
     "lg_spread_tile_seek": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "lg_topk_lists_merge_f64": (ctypes.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
@@ -109,14 +92,36 @@ SIGNATURES = {
     "lg_bound_prep_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "lg_score_chunk_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp,
                                             _vp, _i32, _vp]),
-    "lg_row_norms_f64": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "lg_rec_hits": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     "lg_rec_pair_overlap": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
     "lg_rec_intra_similarity_f64": (
         ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _i64, _vp, _vp]),
 }
 
+# the test-reference entry points (include/lgcnhs_ref.h), exported only by
+# lib/liblgcnhs_ref.so: never bound to the product library
+REF_LIB_PATH = os.path.join(PKG_DIR, "lib", "liblgcnhs_ref.so")
+REF_SIGNATURES = {
+    "lg_spread_tile_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "lg_spread_tile_bound": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "lg_spread_tile_rows_ws_bytes": (_sz, [_i64]),
+    "lg_spread_tile_rows_f64": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp,
+         _vp, _sz, _vp],
+    ),
+    "lg_spread_tile_resource_f64": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp],
+    ),
+    "lg_tile_topk_f64": (
+        ctypes.c_int,
+        [_vp, _i64, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp],
+    ),
+}
+
 _lib = None
+_ref = None
 _lock = threading.Lock()
 
 
@@ -145,6 +150,32 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 def lib() -> ctypes.CDLL:
     return _lib if _lib is not None else load_library()
+
+
+def ref_lib() -> ctypes.CDLL:
+    """The test-reference build (lib/liblgcnhs_ref.so: the product library plus the
+    per-tile reference paths of include/lgcnhs_ref.h), for tests only; its entry points
+    report errors through its own lg_last_error (use ref_check)."""
+    global _ref
+    with _lock:
+        if _ref is None:
+            if not os.path.exists(REF_LIB_PATH):
+                raise RuntimeError(f"test-reference library not found at {REF_LIB_PATH}")
+            r = ctypes.CDLL(REF_LIB_PATH)
+            for name, (res, args) in {**SIGNATURES, **REF_SIGNATURES}.items():
+                fn = getattr(r, name)
+                fn.restype = res
+                fn.argtypes = args
+            if r.lg_abi_version() != ABI_VERSION:
+                raise RuntimeError("liblgcnhs_ref ABI mismatch")
+            _ref = r
+        return _ref
+
+
+def ref_check(status: int, what: str) -> None:
+    if status != LG_OK:
+        msg = ref_lib().lg_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
 
 
 def check(status: int, what: str) -> None:

@@ -407,7 +407,7 @@ def exchange_topk(vals: torch.Tensor, idxs: torch.Tensor, rank: int, world: int,
 
 def sharded_spread_topk(A, lam: float, k: int, excl, drop: bool = True, eu=None, ei=None,
                         rank: int = 0, world: int = 1, group=None, tile: int = 2048,
-                        scratch_bytes: int = 16 << 30, local_fn=None, merge_fn=None,
+                        local_fn=None, merge_fn=None,
                         stats: dict | None = None):
     """The LGCNHS recommendation (model/SpreadLightGCN/model.py:122-153 + recommend.py:18-52)
     over `world` GPUs, sharded by ITEM range: rank r builds only its own tiles of W
@@ -423,8 +423,7 @@ def sharded_spread_topk(A, lam: float, k: int, excl, drop: bool = True, eu=None,
     merge_fn = merge_fn or ops.merge_topk_lists
     i0, i1 = item_range(A.n_items, tile, rank, world)
     kw = {} if stats is None else {"stats": stats}
-    v, i = local_fn(A, lam, k, excl, drop, eu, ei, tile=tile, scratch_bytes=scratch_bytes,
-                    items=slice(i0, i1), **kw)
+    v, i = local_fn(A, lam, k, excl, drop, eu, ei, tile=tile, items=slice(i0, i1), **kw)
     u0, u1 = user_block(A.n_users, rank, world)
     if world == 1:
         return (u0, u1), v, i

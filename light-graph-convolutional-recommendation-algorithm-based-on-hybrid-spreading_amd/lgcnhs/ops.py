@@ -14,8 +14,6 @@ spread_recommend   dense or tiled, whichever fits  model/SpreadMethod/recommend.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -332,18 +330,6 @@ def spread_topk(A: Interactions, W: torch.Tensor, k: int, excl: RowSets | None,
 
 
 # ------------------------------------------------------------------- factored spreading
-def hybrid_factors(k_item: torch.Tensor, lam: float):
-    """(alpha, beta) = (k_i^(1-lambda), k_i^lambda), the HybridS degree factors."""
-    k_item = k_item.contiguous().to(torch.float64)
-    n = k_item.shape[0]
-    alpha = torch.empty(n, dtype=torch.float64, device=k_item.device)
-    beta = torch.empty_like(alpha)
-    N.check(N.lib().lg_hybrid_factors_f64(N.ptr(k_item), n, float(lam), N.ptr(alpha),
-                                          N.ptr(beta), N.stream_handle(k_item.device)),
-            "lg_hybrid_factors_f64")
-    return alpha, beta
-
-
 INV_TAB = 512      # degree classes cached in LDS by the walk (csrc/spread_tiled.hip)
 MAX_CLASSES = 0x7FFF   # P slot words keep bit 31 clear (it marks V entries)
 LINE_SLOTS, LINE_ENTS = 31, 7   # P slots / V entries in a row's 128-byte line
@@ -411,15 +397,15 @@ class TileWeights:
     (lg_spread_tile_rows_f64: one 128-byte line per item row at 128 * i, plus overflow runs;
     P rows = the (user, item) pairs behind the row as 4-byte slots, V rows = the merged fp64
     general_W values of hub items). The tile itself is lambda-independent; ``lam`` sets the
-    HybridScale that resource() applies. build() moves to the next tile; the buffers are
+    HybridScale the walk applies. build() moves to the next tile; the buffers are
     reused and grown on demand. ``vthr``: rows with more pairs are V rows (default: the tile
-    width; LGCNHS_V_THRESHOLD overrides).
+    width).
 
-    Tiles are built ``group`` at a time (default 8, LGCNHS_TILE_GROUP; 1 = the per-tile
-    passes lg_spread_tile_cursor / _bound / _rows_f64): lg_spread_group_cursor / _bound /
-    _rows_f64 visit each (item row, user) pair once per group instead of once per tile and
-    write the group's tiles side by side; build(j0) of a tile inside the built group only
-    selects it. Either way every tile's words are the same bit for bit."""
+    Tiles are built ``group`` at a time (1..8, default 8): lg_spread_group_cursor / _bound /
+    _units / _rows_f64 visit each (item row, user) pair once per group instead of once per
+    tile and write the group's tiles side by side; build(j0) of a tile inside the built
+    group only selects it. Every tile's words are those of the per-tile reference build
+    (include/lgcnhs_ref.h) bit for bit (tests/test_gpu_spread_tiled.py)."""
 
     def __init__(self, A: Interactions, lam: float, tile: int, vthr: int | None = None,
                  group: int | None = None):
@@ -429,44 +415,42 @@ class TileWeights:
         dev = A.k_item.device
         self.dev = dev
         if vthr is None:
-            vthr = int(os.environ.get("LGCNHS_V_THRESHOLD", "0")) or self.tile
+            vthr = self.tile
         self.vthr = max(LINE_SLOTS, int(vthr))
         if group is None:
-            group = int(os.environ.get("LGCNHS_TILE_GROUP", "8"))
+            group = 8
         if not 1 <= group <= 8:
             raise ValueError(f"group {group} not in [1, 8]")
-        if group > 1 and self.vthr > 65535:
-            raise ValueError(f"vthr {self.vthr} > 65535 needs group=1")
+        if self.vthr > 65535:
+            raise ValueError(f"vthr {self.vthr} > 65535 (the group build counts 16-bit)")
         I = A.n_items
         self.group = int(min(group, max(1, -(-I // self.tile))))
         S = self.group
         self.cur = A.by_user.rowptr[:-1].contiguous().clone()
         self.end = torch.empty_like(self.cur)
-        if S == 1:
-            self.counts = torch.empty(A.n_users, dtype=torch.uint16, device=dev)
-        else:  # 8 uint16 per user (one 16-byte load) + the rows pass's 16-byte records
-            if int(A.by_user.rowptr[-1]) >= 1 << 32:
-                raise ValueError("more than 2^32 interactions: use group=1")
-            self.counts = torch.empty((A.n_users, 8), dtype=torch.uint16, device=dev)
-            self.rec = torch.empty((A.n_users, 4), dtype=torch.int32, device=dev)
+        # 8 uint16 per user (one 16-byte load) + the rows pass's 16-byte records
+        if int(A.by_user.rowptr[-1]) >= 1 << 32:
+            raise ValueError("more than 2^32 interactions: the group build's positions are "
+                             "32-bit")
+        self.counts = torch.empty((A.n_users, 8), dtype=torch.uint16, device=dev)
+        self.rec = torch.empty((A.n_users, 4), dtype=torch.int32, device=dev)
         self.inv_deg = torch.empty(A.n_users, dtype=torch.float64, device=dev)
         N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,
                                           N.ptr(self.inv_deg), N.stream_handle(dev)),
                 "lg_inv_degree_f64")
         self.user_cls, self.inv_cls = degree_classes(A.by_user.degrees())
         self.g_bound = torch.empty((S, I), dtype=torch.int64, device=dev)
-        if S > 1:  # run units per (tile, row), their flat inclusive scan, the tiles' ends
-            self.g_units = torch.empty(S * I, dtype=torch.int64, device=dev)
-            self.g_incl = torch.empty(max(1, S * I), dtype=torch.int64, device=dev)
-            self._tile_ends = torch.arange(1, S + 1, dtype=torch.int64, device=dev) * I - 1
-            self._ends_host = torch.empty(S, dtype=torch.int64).pin_memory()
-            self._ends_ev = torch.cuda.Event()
+        # run units per (tile, row), their flat inclusive scan, the tiles' ends
+        self.g_units = torch.empty(S * I, dtype=torch.int64, device=dev)
+        self.g_incl = torch.empty(max(1, S * I), dtype=torch.int64, device=dev)
+        self._tile_ends = torch.arange(1, S + 1, dtype=torch.int64, device=dev) * I - 1
+        self._ends_host = torch.empty(S, dtype=torch.int64).pin_memory()
+        self._ends_ev = torch.cuda.Event()
         # I + 1 lines per tile: line I (the walk's padding row) stays all zero
         self.g_lines = torch.empty((S, (I + 1) * 32), dtype=torch.int32, device=dev)
         self.g_lines[:, I * 32:].zero_()
         self.g_row_len = torch.empty((S, max(1, I)), dtype=torch.int32, device=dev)
-        ws = (N.lib().lg_spread_tile_rows_ws_bytes(I) if S == 1
-              else N.lib().lg_spread_group_rows_ws_bytes(I, S))
+        ws = N.lib().lg_spread_group_rows_ws_bytes(I, S)
         self.ws = torch.empty(max(1, ws), dtype=torch.uint8, device=dev)
         self.g_ovf = torch.zeros(64 * 4, dtype=torch.int32, device=dev)
         self._grp = None  # (first item, [widths], [ovf bases], [overflow units]) built
@@ -570,31 +554,6 @@ class TileWeights:
         A, I, L = self.A, self.A.n_items, N.lib()
         strm = N.stream_handle(self.dev)
         nt = len(widths)
-        if self.group == 1:  # the per-tile passes (their run placement by torch ops)
-            N.check(L.lg_spread_tile_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
-                                            A.n_users, j0 + widths[0], N.ptr(self.cur),
-                                            N.ptr(self.end), N.ptr(self.counts), strm),
-                    "lg_spread_tile_cursor")
-            N.check(L.lg_spread_tile_bound(N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), I,
-                                           N.ptr(self.counts), N.ptr(self.g_bound), strm),
-                    "lg_spread_tile_bound")
-            b = self.g_bound[0]
-            hub = b > self.vthr
-            units = _run_units(torch.where(hub, torch.clamp(b, max=widths[0]), b), hub)
-            cum = torch.cumsum(units, 0)
-            ovf_ptr = cum - units
-            totals = [int(cum[-1]) if I else 0]  # host sync: sizes the overflow runs
-            bases = [0]
-            self._grow_ovf(totals[0])
-            N.check(L.lg_spread_tile_rows_f64(
-                N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
-                N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur),
-                N.ptr(self.counts), j0, self.tile, N.ptr(self.g_bound), self.vthr,
-                N.ptr(ovf_ptr), N.ptr(self.g_lines), N.ptr(self.g_ovf),
-                N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
-                "lg_spread_tile_rows_f64")
-            self._grp = (j0, widths, bases, totals)
-            return
         # group: cursors, bounds, run units and their inclusive scan all on the device; one
         # event wait for the tiles' unit totals (to size ovf), then the rows
         N.check(L.lg_spread_group_cursor(N.ptr(A.by_user.rowptr), N.ptr(A.by_user.col),
@@ -658,42 +617,12 @@ class TileWeights:
             used = _run_units(ln, hub)
             self.bytes_read += 128 * self.row_uses.sum() + 16 * (self.row_uses * used).sum()
 
-    def resource(self, u0: int, u1: int, out: torch.Tensor,
-                 scale: HybridScale | None = None) -> torch.Tensor:
-        """out[u - u0][j - j0] = F[u][j] for users [u0, u1) and the current tile."""
-        A = self.A
-        sc = scale if scale is not None else self.scale
-        N.check(N.lib().lg_spread_tile_resource_f64(
-            N.ptr(A.by_user.rowptr[u0:]), N.ptr(A.by_user.col), N.ptr(sc.ra_edge), u1 - u0,
-            N.ptr(self.lines), N.ptr(self.ovf), A.n_items, N.ptr(sc.rb), N.ptr(self.inv_cls),
-            self.j0,
-            self.tile, self.width, N.ptr(out), out.stride(0), N.stream_handle(self.dev)),
-            "lg_spread_tile_resource_f64")
-        return out
-
-
-def tile_topk(F: torch.Tensor, j0: int, n_cols: int, k: int, vals: torch.Tensor,
-              idxs: torch.Tensor, first: bool, excl: RowSets | None = None, drop: bool = True,
-              eu: torch.Tensor | None = None, ei: torch.Tensor | None = None) -> None:
-    """Merge columns [j0, j0 + n_cols) of (G *) F into the running lists vals/idxs."""
-    n = F.shape[0]
-    d = 0
-    if eu is not None:
-        eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
-        d = eu.shape[1]
-    N.check(N.lib().lg_tile_topk_f64(
-        N.ptr(F), F.stride(0), n, j0, n_cols, N.ptr(eu), N.ptr(ei), d,
-        N.ptr(excl.rowptr if excl else None), N.ptr(excl.col if excl else None),
-        N.LG_EXCL_DROP if drop else N.LG_EXCL_NONE, int(k), int(bool(first)), N.ptr(vals),
-        N.ptr(idxs), N.stream_handle(F.device)), "lg_tile_topk_f64")
-
-
 def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       drop: bool = True, eu: torch.Tensor | None = None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
-                      tile: int = 2048, scratch_bytes: int = 4 << 30,
-                      items: slice | None = None, fused: bool | None = None,
-                      stats: dict | None = None, count_paths: bool = False):
+                      tile: int = 2048, items: slice | None = None,
+                      stats: dict | None = None, count_paths: bool = False,
+                      col_bounds: bool = True, **_):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). The values of spread_topk(A,
     hybrid_weight(spread_general(A), A.k_item, lam), ...) within a few ulp (the walk's
@@ -706,10 +635,9 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     columns, so only those whose bound times F can beat the list's k-th value get the exact
     fp32 score chain. ``users`` restricts the output to a row range; ``items`` restricts the
     candidates to an item range (the lists of disjoint item ranges merge, with
-    merge_topk_lists, into the full lists: the multi-GPU item shard). fused=False keeps the
-    two-kernel form (F columns of a span of tiles written to a [users, span] scratch of
-    ``scratch_bytes``, then lg_tile_topk_f64; the same F values, so the same lists).
-    ``stats`` (optional dict) receives, on the fused path, the HIP-event times of the tile
+    merge_topk_lists, into the full lists: the multi-GPU item shard). (The two-kernel form
+    -- F written per tile, then a top-K merge -- is a test reference, tests/_ref_paths.py.)
+    ``stats`` (optional dict) receives the HIP-event times of the tile
     builds / score bounds / walk launches (t_*_ms, walk_launches) and the walk's (user, item)
     rows per launch; with ``count_paths`` also "w_paths": the paths the walk adds (sum over
     tiles and users u of sum_{i in items(u)} the pairs (P) / entries (V) of row i in the
@@ -731,51 +659,38 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
         tw.seek(i0)
     ex = excl.slice_rows(u0, u1) if excl is not None else None
     eu_r = None if eu is None else eu[u0:u1]
-    if fused is None:
-        fused = True
     if stats is not None and count_paths:
         _count_rows(tw, A, u0, u1)
-    if fused:
-        walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile)
-        evs = [] if stats is not None else None
-        for j0 in range(i0, i1, tile):
-            if evs is not None:  # per-tile HIP events on the launch stream: build / bounds / walk
-                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-                e[0].record()
-            tw.build(j0, stop=i1)
-            if evs is not None:
-                e[1].record()
-            bnd = walk.bounds(j0, tw.width)
-            if evs is not None:
-                e[2].record()
-            walk.step(tw.lines, tw.ovf, tw.inv_cls, tw.scale, j0, tile, tw.width, j0 == i0, bnd)
-            if evs is not None:
-                e[3].record()
-                evs.append(e)
-        vals.copy_(walk.vals)
-        idxs.copy_(walk.idxs)
-        if evs:
-            torch.cuda.synchronize(dev)
-            stats["t_build_ms"] = stats.get("t_build_ms", 0.0) + sum(e[0].elapsed_time(e[1]) for e in evs)
-            stats["t_bounds_ms"] = stats.get("t_bounds_ms", 0.0) + sum(e[1].elapsed_time(e[2]) for e in evs)
-            stats["t_walk_ms"] = stats.get("t_walk_ms", 0.0) + sum(e[2].elapsed_time(e[3]) for e in evs)
-            stats["walk_launches"] = stats.get("walk_launches", 0) + len(evs)
-            stats["walk_ms_list"] = stats.get("walk_ms_list", []) + [e[2].elapsed_time(e[3]) for e in evs]
-            stats["user_items"] = stats.get("user_items", 0) + len(evs) * int(
-                A.by_user.rowptr[u1] - A.by_user.rowptr[u0])
-            stats["users"] = n
-            stats["qstride"] = 0 if walk.d == 0 or walk.qbuf is None else walk.qbuf.shape[1]
-            stats["nch"] = -(-tile // 64) if walk.d else 0
-    else:
-        span = max(tile, scratch_bytes // (n * 8) // tile * tile)
-        span = min(span, -(-(i1 - i0) // tile) * tile)
-        F = torch.empty((n, span), dtype=torch.float64, device=dev)
-        for s0 in range(i0, i1, span):
-            s1 = min(i1, s0 + span)
-            for j0 in range(s0, s1, tile):
-                tw.build(j0, stop=i1)
-                tw.resource(u0, u1, F[:, j0 - s0:])
-            tile_topk(F, s0, s1 - s0, k, vals, idxs, s0 == i0, ex, drop, eu_r, ei)
+    walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile, col_bounds)
+    evs = [] if stats is not None else None
+    for j0 in range(i0, i1, tile):
+        if evs is not None:  # per-tile HIP events on the launch stream: build / bounds / walk
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record()
+        tw.build(j0, stop=i1)
+        if evs is not None:
+            e[1].record()
+        bnd = walk.bounds(j0, tw.width)
+        if evs is not None:
+            e[2].record()
+        walk.step(tw.lines, tw.ovf, tw.inv_cls, tw.scale, j0, tile, tw.width, j0 == i0, bnd)
+        if evs is not None:
+            e[3].record()
+            evs.append(e)
+    vals.copy_(walk.vals)
+    idxs.copy_(walk.idxs)
+    if evs:
+        torch.cuda.synchronize(dev)
+        stats["t_build_ms"] = stats.get("t_build_ms", 0.0) + sum(e[0].elapsed_time(e[1]) for e in evs)
+        stats["t_bounds_ms"] = stats.get("t_bounds_ms", 0.0) + sum(e[1].elapsed_time(e[2]) for e in evs)
+        stats["t_walk_ms"] = stats.get("t_walk_ms", 0.0) + sum(e[2].elapsed_time(e[3]) for e in evs)
+        stats["walk_launches"] = stats.get("walk_launches", 0) + len(evs)
+        stats["walk_ms_list"] = stats.get("walk_ms_list", []) + [e[2].elapsed_time(e[3]) for e in evs]
+        stats["user_items"] = stats.get("user_items", 0) + len(evs) * int(
+            A.by_user.rowptr[u1] - A.by_user.rowptr[u0])
+        stats["users"] = n
+        stats["qstride"] = 0 if walk.d == 0 or walk.qbuf is None else walk.qbuf.shape[1]
+        stats["nch"] = -(-tile // 64) if walk.d else 0
     if stats is not None and count_paths:
         stats["w_paths"] = stats.get("w_paths", 0) + int(tw.paths_read)
         stats["w_bytes"] = stats.get("w_bytes", 0) + int(tw.bytes_read)
@@ -856,7 +771,8 @@ class TileWalk:
     can share them."""
 
     def __init__(self, A: Interactions, u0: int, u1: int, i0: int, k: int,
-                 ex: RowSets | None, eu=None, ei=None, tile: int = 2048):
+                 ex: RowSets | None, eu=None, ei=None, tile: int = 2048,
+                 col_bounds: bool = True):
         self.A, self.u0, self.u1, self.i0, self.k, self.ex = A, u0, u1, i0, int(k), ex
         self.n = u1 - u0
         self.dev = A.k_item.device
@@ -872,9 +788,9 @@ class TileWalk:
             self.ib, self.inorm = bound_operands(self.ei)
             self.gbuf = torch.empty(self.n * -(-int(tile) // 64), dtype=torch.float32,
                                     device=self.dev)
-            # per-column 8-bit bounds (LGCNHS_COL_BOUNDS=0: chunk bounds only)
+            # per-column 8-bit bounds (col_bounds=False: chunk bounds only)
             self.qbuf = None
-            if os.environ.get("LGCNHS_COL_BOUNDS", "1") != "0":
+            if col_bounds:
                 self.qbuf = torch.empty((self.n, -(-int(tile) // 256) * 256),
                                         dtype=torch.uint8, device=self.dev)
         self.ex_cur = None

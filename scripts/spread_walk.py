@@ -18,9 +18,10 @@ ap.add_argument("--tiles", type=int, default=16)
 ap.add_argument("--tile", type=int, default=2048)
 ap.add_argument("--workload", default="c5-d64")
 ap.add_argument("--reps", type=int, default=2)
-ap.add_argument("--unfused", action="store_true")
 ap.add_argument("--no-g", action="store_true", help="no G factor (SpreadMethod)")
 ap.add_argument("--count", action="store_true", help="count paths / row bytes (extra work)")
+ap.add_argument("--no-col-bounds", action="store_true",
+                help="chunk score bounds only (no per-column 8-bit bounds)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
@@ -30,13 +31,13 @@ del keys
 g = torch.Generator(device=dev).manual_seed(42)
 eu = torch.randn(U, D, device=dev, generator=g) * 0.1
 ei = torch.randn(I, D, device=dev, generator=g) * 0.1
-kw = {} if a.no_g else {"eu": eu, "ei": ei}
+kw = {} if a.no_g else {"eu": eu, "ei": ei, "col_bounds": not a.no_col_bounds}
 for rep in range(a.reps):
     torch.cuda.synchronize()
     t = time.time()
     st = {}
-    vals, idxs = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile, fused=not a.unfused,
-                          items=slice(0, a.tiles * a.tile), scratch_bytes=32 << 30,
+    vals, idxs = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile,
+                          items=slice(0, a.tiles * a.tile),
                           stats=st if rep == 0 else None, count_paths=a.count, **kw)
     torch.cuda.synchronize()
     dt = time.time() - t

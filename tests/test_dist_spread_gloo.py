@@ -34,7 +34,7 @@ def _problem(U, I, n, seed, lam):
 
 
 def _cpu_local(F, ex_rowptr, ex_col):
-    def local(A, lam, k, excl, drop, eu, ei, tile, scratch_bytes, items):
+    def local(A, lam, k, excl, drop, eu, ei, tile, items):
         Fm = np.full_like(F, -np.inf)
         Fm[:, items.start:items.stop] = F[:, items.start:items.stop]
         v, i = O.rows_topk(Fm, k, ex_rowptr, ex_col, drop)

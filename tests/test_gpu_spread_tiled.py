@@ -4,13 +4,14 @@ relative of the dense path (lg_spread_general_f64 -> lg_hybrid_weight_f64 ->
 lg_spread_resource_f64, itself pinned to the reference's numpy results in
 test_gpu_spread.py; the walk sums each column's paths in its own fixed order), its top-k
 lists equal to the dense path's except rounding-level ties; plus the reference fixture for
-the LGCNHS recommendation. Tiled-vs-tiled properties (user / item shards, fused vs
-two-kernel, lambda sweep) are bitwise."""
+the LGCNHS recommendation. Tiled-vs-tiled properties (user / item shards, fused vs the
+two-kernel reference of tests/_ref_paths.py, lambda sweep) are bitwise."""
 import numpy as np
 import pytest
 import torch
 
 from _compare import compare_lists_close, compare_topk_sets
+import _ref_paths as RP
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -64,7 +65,7 @@ def test_tile_weights_and_resource(zipf, lam):
         ovf_seen |= bool(((tw.bound > 31) & ~tw.is_hub).any())
         Wt = _dense_tile(tw, I)
         assert np.array_equal(Wt.view(np.uint64), gW[:, j0:j0 + tw.width].view(np.uint64))
-        tw.resource(0, U, Fb)
+        RP.resource(tw, 0, U, Fb)
         _close(Fb[:, :tw.width].cpu().numpy(), F[:, j0:j0 + tw.width])
     assert ovf_seen, "the graph should exercise P rows with overflow runs"
     if zipf:
@@ -83,7 +84,7 @@ def test_group_build_equals_per_tile(zipf, tile, group, vthr):
     U, I = 700, 900
     A = _inter(U, I, 30000 if zipf else 12000, seed=5, zipf=zipf)
     stop = I - 37
-    a = ops.TileWeights(A, 0.5, tile, vthr=vthr, group=1)
+    a = RP.PerTileWeights(A, 0.5, tile, vthr=vthr)
     b = ops.TileWeights(A, 0.5, tile, vthr=vthr, group=group)
     hub_seen = ovf_seen = False
     for j0 in range(0, stop, tile):
@@ -118,14 +119,15 @@ def test_spread_topk_tiled_equals_dense(k, tile, mode):
     W = ops.hybrid_weight(ops.spread_general(A), A.k_item, lam)
     kw = dict(eu=eu if use_g else None, ei=ei if use_g else None)
     v0, i0 = ops.spread_topk(A, W, k, A.by_user, drop=drop, **kw)
-    # fused resource + top-K (the reference for the others, bit for bit); unfused with
-    # scratch for one tile (span = tile) and for several tiles per top-k merge
-    vf, if_ = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile, fused=True, **kw)
+    # the fused walk; the two-kernel reference (tests/_ref_paths.py: F written by the
+    # reference walk, then lg_tile_topk_f64) with scratch for one tile (span = tile) and for
+    # several tiles per top-k merge gives the same lists bit for bit
+    vf, if_ = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile, **kw)
     compare_lists_close(vf.cpu().numpy(), if_.cpu().numpy(), v0.cpu().numpy(), i0.cpu().numpy(),
                         label=f"tiled vs dense k={k} tile={tile} {mode}")
     for scratch in (1, 3 * U * 8 * tile):
-        v1, i1 = ops.spread_topk_tiled(A, lam, k, A.by_user, drop=drop, tile=tile,
-                                       scratch_bytes=scratch, fused=False, **kw)
+        v1, i1 = RP.spread_topk_two_kernel(A, lam, k, A.by_user, drop=drop, tile=tile,
+                                           scratch_bytes=scratch, **kw)
         assert torch.equal(i1, if_), scratch
         assert torch.equal(v1.view(torch.int64), vf.view(torch.int64)), scratch
 
@@ -283,10 +285,10 @@ def test_fused_dims_and_wide_k(d, k):
     eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
     ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
     for items in (None, slice(130, 470)):
-        ref = ops.spread_topk_tiled(A, 0.6, k, A.by_user, eu=eu, ei=ei, tile=128,
-                                    fused=False, scratch_bytes=1, items=items)
+        ref = RP.spread_topk_two_kernel(A, 0.6, k, A.by_user, eu=eu, ei=ei, tile=128,
+                                        scratch_bytes=1, items=items)
         got = ops.spread_topk_tiled(A, 0.6, k, A.by_user, eu=eu, ei=ei, tile=128,
-                                    items=items, fused=True)
+                                    items=items)
         assert torch.equal(got[1], ref[1])
         assert torch.equal(got[0].view(torch.int64), ref[0].view(torch.int64))
 
@@ -309,8 +311,9 @@ def test_spread_stats_count_path_updates(fused):
     tile = 64
     for users, items in ((slice(0, U), slice(0, I)), (slice(20, 90), slice(77, 301))):
         st = {}
-        ops.spread_topk_tiled(A, 0.5, 10, A.by_user, tile=tile, users=users, items=items,
-                              fused=fused, stats=st, count_paths=True)
+        fn = ops.spread_topk_tiled if fused else RP.spread_topk_two_kernel
+        fn(A, 0.5, 10, A.by_user, tile=tile, users=users, items=items, stats=st,
+           count_paths=True)
         uses = Ad[users].sum(0)
         paths = nbytes = 0
         for j0 in range(items.start, items.stop, tile):
@@ -355,7 +358,7 @@ def test_tile_resource_persistent_waves(zipf):
     first = None
     for j0 in range(0, I, tile):
         tw.build(j0)
-        tw.resource(0, U, Fb)
+        RP.resource(tw, 0, U, Fb)
         Ft = Fb[:, :tw.width].cpu().numpy()
         _close(Ft, F[:, j0:j0 + tw.width])
         if first is None:
@@ -364,7 +367,7 @@ def test_tile_resource_persistent_waves(zipf):
     Fb2 = torch.empty((2500, tile), dtype=torch.float64, device=DEV)
     tw2 = ops.TileWeights(A, 0.5, tile)
     tw2.build(0)
-    tw2.resource(1000, 3500, Fb2)
+    RP.resource(tw2, 1000, 3500, Fb2)
     assert np.array_equal(Fb2[:, :tw2.width].cpu().numpy().view(np.uint64),
                           first[1000:3500].view(np.uint64))
 

@@ -9,8 +9,8 @@ import pytest
 from conftest import PKG, REPO
 
 
-def declared_functions():
-    src = open(os.path.join(REPO, "include", "lgcnhs.h")).read()
+def declared_functions(header="lgcnhs.h"):
+    src = open(os.path.join(REPO, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(lg_[a-z0-9_]+)\s*\(", src)))
 
@@ -18,6 +18,21 @@ def declared_functions():
 def test_header_and_binding_agree():
     from lgcnhs import _native as N
     assert declared_functions() == sorted(N.SIGNATURES)
+    assert declared_functions("lgcnhs_ref.h") == sorted(N.REF_SIGNATURES)
+
+
+def test_reference_paths_only_in_the_reference_build():
+    """The per-tile reference paths (include/lgcnhs_ref.h) are exported by
+    lib/liblgcnhs_ref.so for the tests and NOT by the product library."""
+    from lgcnhs import _native as N
+    prod = N.load_library()
+    ref = N.ref_lib()
+    for name in declared_functions("lgcnhs_ref.h"):
+        assert not hasattr(prod, name), name
+        assert hasattr(ref, name), name
+    for name in declared_functions():
+        assert hasattr(ref, name), name
+    assert ref.lg_abi_version() == prod.lg_abi_version() == N.ABI_VERSION
 
 
 def test_library_exports_every_symbol():
