@@ -282,7 +282,7 @@ def time_exchange(prop, shard, D, world, dev, reps=5):
     dt = float(t.item())
     recv = (world - 1) / world * shard.n_pad * D * 4
     return {"allgather_ms_per_layer": dt * 1e3, "recv_GBps_per_gpu": recv / dt / 1e9,
-            "recv_bytes_per_gpu": recv}
+            "recv_bytes_per_gpu": recv, "pad_ratio": shard.pad_ratio}
 
 
 def bench_small_config(dev, k):

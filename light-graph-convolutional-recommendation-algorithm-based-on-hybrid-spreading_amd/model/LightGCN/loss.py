@@ -46,17 +46,20 @@ def _exact_free_items(u: torch.Tensor, keys: torch.Tensor, num_items: int, gener
         raise ValueError(f"user {bad} has interacted with every item: no negative to sample")
     r = (torch.rand(uu.shape, device=uu.device, generator=generator) * free).long()
     r = torch.minimum(r, free - 1)
-    out = []
-    for t in range(uu.numel()):  # few entries: the ones rejection sampling left
-        p = (keys[int(lo[t]):int(hi[t])] - int(uu[t]) * num_items).tolist()
-        c = int(r[t])
-        for x in p:  # the c-th free item: skip every positive at or below the candidate
-            if x <= c:
-                c += 1
-            else:
-                break
-        out.append(c)
-    return torch.tensor(out, dtype=torch.int64, device=u.device)
+    # The r-th free item is r + j, j = the number of the user's positives p_i (ascending,
+    # i = 0, 1, ...) with p_i - i <= r (p_i - i = the free items below p_i, non-decreasing
+    # in i). All entries at once on the device: their positives gathered as segments, the
+    # count by one searchsorted over (entry, p_i - i) keys (two host syncs in all).
+    n = uu.numel()
+    total = int(n_pos.sum())
+    excl = torch.cumsum(n_pos, 0) - n_pos
+    seg = torch.repeat_interleave(torch.arange(n, device=uu.device), n_pos)
+    offs = torch.arange(total, device=uu.device) - excl[seg]
+    g = keys[lo[seg] + offs] - uu[seg] * num_items - offs
+    skey = seg * (num_items + 1) + g
+    j = torch.searchsorted(skey, torch.arange(n, device=uu.device) * (num_items + 1) + r,
+                           right=True) - excl
+    return (r + j).to(device=u.device, dtype=torch.int64)
 
 
 def _negatives(u: torch.Tensor, keys: torch.Tensor, num_items: int, generator=None):

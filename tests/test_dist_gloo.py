@@ -127,7 +127,8 @@ def _worker_zipf(rank, world, port, U, I, users, items, layers, chunks, q, balan
         prop = BipartitePropagation(shard, shard.permute_rows(dis), 8, layers, "cpu",
                                     layer_fn=cpu_layer)
         out = prop.forward(e0, gather_out=True)
-        q.put((rank, shard.nnz, shard.unpermute_rows(out).numpy().copy() if rank == 0 else None))
+        q.put((rank, shard.nnz, shard.unpermute_rows(out).numpy().copy() if rank == 0 else None,
+               shard.pad_ratio))
     finally:
         dist.destroy_process_group()
 
@@ -156,12 +157,32 @@ def test_nnz_balanced_shards_zipf(world):
     nnz = np.array([g[1] for g in sorted(got, key=lambda g: g[0])], np.float64)
     assert nnz.sum() == 2 * users.size
     assert np.abs(nnz - nnz.mean()).max() <= 0.05 * nnz.mean(), nnz
+    # the pieces are capped at 2x the mean piece length: padding (replicated tables and
+    # all-gathered rows beyond n) stays bounded
+    assert max(g[3] for g in got) <= 2.0 + 2 * world * 2 / (U + I), [g[3] for g in got]
     out = [g[2] for g in got if g[0] == 0][0]
     torch.manual_seed(0)
     e0 = torch.randn(U + I, 8) * 0.1
     coo = torch.as_tensor(O.coo_adjacency(U, I, users, items))
     uf, itf = O.lightgcn_forward(coo, e0[:U], e0[U:], 3)
     np.testing.assert_allclose(out, torch.cat([uf, itf]).numpy(), atol=1e-6, rtol=0)
+
+
+def test_piece_bounds_cap_bounds_padding():
+    """A power-law row range whose heavy rows come first: uncapped nnz cuts give the last
+    piece most of the rows (padding ~parts-fold); the cap holds every piece to max_rows x the
+    mean length and still covers the range monotonically."""
+    from lgcnhs.dist import piece_bounds
+    deg = np.concatenate([np.full(50, 2000), np.ones(9950, np.int64)])
+    rowptr = torch.as_tensor(np.concatenate([[0], np.cumsum(deg)]))
+    for parts in (4, 8, 16):
+        free = piece_bounds(rowptr, 0, deg.size, parts, max_rows=0)
+        capped = piece_bounds(rowptr, 0, deg.size, parts)
+        lf = np.diff(free)
+        lc = np.diff(capped)
+        assert lf.max() > 2 * deg.size / parts  # the pathology the cap removes
+        assert capped[0] == 0 and capped[-1] == deg.size and (lc >= 0).all()
+        assert lc.max() <= -(-int(2.0 * deg.size) // parts)
 
 
 def test_piece_bounds_balance_and_rows():
