@@ -1056,8 +1056,9 @@ __host__ __device__ constexpr size_t walk_wave_bytes(int tile) {
   return ((size_t)acc_cols(tile) * 8 + (size_t)kOvfList * 12 + 15) & ~(size_t)15;
 }
 __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
-  // class table + the block's rb maxima + rb of the tile's columns
-  return (size_t)kInvTab * 8 + 16 * 8 + (size_t)tile * 8;
+  // class table + the block's rb maxima + rb of the tile's columns + its 64-column chunks'
+  // rb maxima
+  return (size_t)kInvTab * 8 + 16 * 8 + (size_t)((tile + 1) & ~1) * 8 + 64 * 8;
 }
 
 __device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
@@ -1142,7 +1143,10 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   double *s_inv = lds;  // at LDS address 0 (the fast decode indexes it with class * 8)
   double *s_red = s_inv + kInvTab;
   double *s_rb = s_red + 16;  // rb of the tile's columns (0 past the width)
-  char *mine = reinterpret_cast<char *>(s_rb + tile) +
+  // per 64-column chunk: the largest rb (G screen, tile <= 4096); the waves' areas after it
+  // (16-byte aligned: the tile's rb padded to an even count)
+  double *s_rbc = s_rb + ((tile + 1) & ~1);
+  char *mine = reinterpret_cast<char *>(s_rbc + 64) +
                (size_t)wave * walk_wave_bytes<MODE, D, M>(tile);
   double *acc = reinterpret_cast<double *>(mine);
   const uint32_t acc_base = (uint32_t)(uintptr_t)(lds_f64 *)acc;
@@ -1164,6 +1168,15 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   if (lane == 0) s_red[wave] = rmax;
   for (int j = lane; j < acc_cols(tile); j += 64) acc[j] = 0.0;
   __syncthreads();
+  if (MODE == MODE_TOPK && D > 0) {
+    for (int c = wave; 64 * c < tile && c < 64; c += nw) {
+      double m = s_rb[64 * c + lane < tile ? 64 * c + lane : 0];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+      if (lane == 0) s_rbc[c] = m;
+    }
+    __syncthreads();
+  }
   rmax = 0.0;
   for (int w = 0; w < nw; ++w) rmax = fmax(rmax, s_red[w]);
   // acc * rb_j > tau  implies  acc * rb_max * (1 + 2^-50) > tau (rounding of both products)
@@ -1474,7 +1487,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       // The scan, 512 columns per iteration: lane l takes columns c0 + 4l .. + 3 and
       // c0 + 256 + 4l .. + 3 (ds_read_b128 x 4). A column can enter only if
       //   no G:  acc > thr = tau / (rb_max (1 + 2^-50))            (excluded: acc = -inf)
-      //   G:     acc * q * (rb_max (1 + 2^-50) max(gb, 0) / 255) > tau
+      //   G:     acc * q * (rbmax_c (1 + 2^-50) max(gb, 0) / 255) > tau   (c = the chunk)
       // (gb * q / 255 >= the exact score, q = the column's 8-bit bound, 255 without qb; the
       // 2^-50 margin covers every rounding of fl(G fl(acc rb_j)) > tau). The lanes' passing
       // columns form a bit mask that one loop drains (one candidate per lane per round): rb_j,
@@ -1483,8 +1496,10 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       double thr_s = tau / rscale;
       double sc_v = 0.0, bq_v = 0.0;  // per 64-column chunk c in lane c (D > 0)
       if constexpr (D > 0) {
+        // the pre-screen scale of chunk c: its own largest rb (not the tile's), so a column
+        // passes only if acc * q * rbmax_c (1 + 2^-50) gb / 255 > tau
         const double gp = (double)fmaxf(gbv, 0.f);
-        sc_v = rscale * gp * (1.0 / 255.0);
+        sc_v = s_rbc[lane < a.nch ? lane : 0] * (1.0 + 0x1p-50) * gp * (1.0 / 255.0);
         bq_v = gp * (1.0 / 255.0) * (1.0 + 0x1p-50);
       }
       auto q_at = [&](int c0) __attribute__((always_inline)) {  // q dword of column c0 + 4l
