@@ -22,6 +22,8 @@ ap.add_argument("--no-g", action="store_true", help="no G factor (SpreadMethod)"
 ap.add_argument("--count", action="store_true", help="count paths / row bytes (extra work)")
 ap.add_argument("--no-col-bounds", action="store_true",
                 help="chunk score bounds only (no per-column 8-bit bounds)")
+ap.add_argument("--rb-in-bounds", action="store_true",
+                help="per-column bounds carry rb_j / rbmax_c (lg_score_chunk_bound rbeta)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
@@ -31,7 +33,8 @@ del keys
 g = torch.Generator(device=dev).manual_seed(42)
 eu = torch.randn(U, D, device=dev, generator=g) * 0.1
 ei = torch.randn(I, D, device=dev, generator=g) * 0.1
-kw = {} if a.no_g else {"eu": eu, "ei": ei, "col_bounds": not a.no_col_bounds}
+kw = {} if a.no_g else {"eu": eu, "ei": ei, "col_bounds": not a.no_col_bounds,
+                        "rb_in_bounds": a.rb_in_bounds}
 for rep in range(a.reps):
     torch.cuda.synchronize()
     t = time.time()
