@@ -149,6 +149,20 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
                       float mask_value, int32_t k, int32_t n_splits, float *out_val,
                       int64_t *out_idx, void *ws, size_t ws_bytes, lg_stream_t stream);
 
+/* lg_score_topk_f32 with a bf16 MFMA screen (csrc/topk.hip K2s): the same outputs bit for
+ * bit (values, ids, order), computing the exact fp32 chain only for 16-item tiles in which
+ * some user's bf16 product plus umarg[u] can beat its entry threshold. eu_bf16 / ei_bf16:
+ * lg_bound_prep_f32's bf16 copies of eu / ei (16-byte aligned); umarg[u] (fp32, per user)
+ * must be >= 0.00785 ||eu[u]|| max_i ||ei[i]|| (lgcnhs.ops uses 0.0081 with the rounded-up
+ * norms of lg_bound_prep_f32), the bound on |bf16 product - fp32 chain| of gbound.hip.
+ * Workspace and splits as lg_score_topk_f32. */
+int lg_score_topk_screened_f32(const float *eu, const float *ei, const void *eu_bf16,
+                               const void *ei_bf16, const float *umarg, int64_t n_users,
+                               int64_t n_items, int32_t dim, const int64_t *ex_rowptr,
+                               const int32_t *ex_col, float mask_value, int32_t k,
+                               int32_t n_splits, float *out_val, int64_t *out_idx, void *ws,
+                               size_t ws_bytes, lg_stream_t stream);
+
 /* Dense masked score matrix G[u][i] (same score definition and mask as above), written
  * with leading dimension ldg. Replaces getAllocateMat's matmul + masks
  * (model/SpreadLightGCN/model.py:74-104, model/SpreadLightGCNOpti/model.py:139-169). */

@@ -322,6 +322,233 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   }
 }
+// K2s: the same top-K with a bf16 MFMA screen (v_mfma_f32_16x16x32_bf16, 16x the f32
+// MFMA's rate). Per 16-item tile every user's bf16 product plus a rigorous margin m_u
+// (|G_bf16 - G_chain| <= 0.00785 ||u|| ||i||, csrc/gbound.hip; m_u = 0.0081 ||u|| max ||i||
+// >= it) is an upper bound of the exact fp32 chain score. Only a tile where some user's bound
+// beats its entry threshold is recomputed with the f32 MFMA chain of k_score_topk -- the
+// exact scores, bit for bit -- and runs k_score_topk's insertion on them. A tile that is not
+// recomputed holds no score above any threshold, so k_score_topk would have inserted
+// nothing from it either: the lists (values, ids, order) are k_score_topk's exactly. While a
+// user's list can still take the mask value (thr = -inf) every tile is recomputed.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int D, int NG, int M, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
+    const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
+    const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
+    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
+  constexpr int Q = D / 4;   // f32 MFMA steps
+  constexpr int S = D / 32;  // bf16 MFMA k-blocks
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[WAVES][NG][16][CAP];
+  __shared__ int ci[WAVES][NG][16][CAP];
+  __shared__ int exs[WAVES][64];
+
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  const int64_t tile = blockIdx.x / n_splits;
+  const int split = blockIdx.x % n_splits;
+  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
+  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  const int64_t i0 = (int64_t)split * items_per_split;
+  int64_t i1 = i0 + items_per_split;
+  if (i1 > n_items) i1 = n_items;
+  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;
+  const int n_t = (n_valid + 15) / 16;
+
+  float uf[NG][Q];
+  bf16x8 ub[NG][S];
+  float marg[NG];
+  bool uvalid[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
+  int cnt[NG], chk[NG];
+  float tau[NG], thr[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t u = ubase + g * 16 + ul;
+    uvalid[g] = u < n_users;
+    const int64_t uu = uvalid[g] ? u : n_users - 1;
+    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
+    marg[g] = umarg[uu];
+    ex_pos[g] = 0;
+    ex_hi[g] = 0;
+    if (ex_rowptr && uvalid[g]) {
+      ex_pos[g] = ex_rowptr[u];
+      ex_hi[g] = ex_rowptr[u + 1];
+    }
+    cnt[g] = 0;
+    chk[g] = 0;
+    tau[g] = neg_inf<float>();
+    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
+  }
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+
+  // (k_score_topk's lazy exclusion and compaction, unchanged)
+  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
+    const int n = __shfl(cnt[g], u);
+    const int c0 = __shfl(chk[g], u);
+    int64_t pos = __shfl(ex_pos[g], u);
+    const int64_t hi = __shfl(ex_hi[g], u);
+    float *ks = &cs[wave][g][u][0];
+    int *is = &ci[wave][g][u][0];
+    if (n > c0) {
+      while (pos < hi) {
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        const int nin = __popcll(__ballot(x < lim));
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        for (int j = c0 + lane; j < n; j += 64) {
+          const int item = is[j];
+          int a = 0, b = nin;
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) ks[j] = mask_value;
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
+      }
+    }
+    float t;
+    int tid;
+    const int nc = wave_compact<float, M>(ks, is, n, k, t, tid);
+    if (ul == u) {
+      cnt[g] = nc;
+      chk[g] = nc;
+      tau[g] = t;
+      ex_pos[g] = pos;
+      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
+    }
+  };
+  auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    if (__ballot(over) == 0) return;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+      if (need) {
+        wave_sync();
+        while (need) {
+          const int u = __ffsll((long long)need) - 1;
+          need &= need - 1;
+          compact_user(g, u, lim);
+        }
+      }
+    }
+  };
+  // bf16 fragments of tile t: lane (ul, gq) holds item ul's elements 32 s + 8 gq .. + 7
+  auto load_bf = [&](int t, bf16x8 (&fr)[S]) __attribute__((always_inline)) {
+    int64_t it = i0 + 16 * t + ul;
+    it = it < n_items ? it : n_items - 1;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      fr[s] = *reinterpret_cast<const bf16x8 *>(eib + it * D + 32 * s + 8 * gq);
+  };
+  // the exact tile: k_score_topk's f32 chain, then its insertion against thr
+  auto exact_tile = [&](int t) __attribute__((always_inline)) {
+    int64_t it = i0 + 16 * t + ul;
+    it = it < n_items ? it : n_items - 1;
+    float af[Q];
+    load_piece<Q>(ei + it * D + gq * Q, af);
+    f32x4 acc[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < Q; ++s)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
+    const int rel = t * 16 + gq * 4;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (__ballot(max4(acc[g]) > thr[g]) == 0) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = acc[g][r];
+        const bool cand = rel + r < n_valid && sc > thr[g];
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][pos] = sc;
+            ci[wave][g][ul][pos] = (int)i0 + rel + r;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+  };
+
+  const int lim_end = (int)i1;
+  bf16x8 fa[S], fb[S];
+  if (n_t > 0) load_bf(0, fa);
+  if (n_t > 1) load_bf(1, fb);
+  for (int t = 0; t < n_t; ++t) {
+    f32x4 accb[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((t & 1) ? fb[s] : fa[s], ub[g][s],
+                                                          accb[g], 0, 0, 0);
+    }
+    // tile t + 2 into the buffer tile t just left
+    if (t + 2 < n_t) {
+      if (t & 1) load_bf(t + 2, fb);
+      else load_bf(t + 2, fa);
+    }
+    bool hit = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) hit |= max4(accb[g]) + marg[g] > thr[g];
+    if (__ballot(hit)) {
+      exact_tile(t);
+      const int l = (int)i0 + (t + 1) * 16;
+      maybe_compact(l < lim_end ? l : lim_end);
+    }
+  }
+
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t user = ubase + g * 16 + u;
+      if (user >= n_users) break;
+      compact_user(g, u, lim_end);
+      const int nc = __shfl(cnt[g], u);
+      for (int e = lane; e < k; e += 64) {
+        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
+        const int id = e < nc ? ci[wave][g][u][e] : -1;
+        if (n_splits == 1) {
+          out_val[user * k + e] = v;
+          out_idx[user * k + e] = id;
+        } else {
+          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          part_val[o] = v;
+          part_idx[o] = id;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
 // Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
 template <int M>
 __global__ __launch_bounds__(256) void k_topk_merge(const float *__restrict__ part_val,
@@ -483,6 +710,29 @@ static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_use
                             stream);
 }
 
+template <int D>
+static void dispatch_topk_screen(int M, const float *eu, const float *ei, const __bf16 *eub,
+                                 const __bf16 *eib, const float *umarg, int64_t n_users,
+                                 int64_t n_items, const int64_t *ex_rowptr,
+                                 const int32_t *ex_col, float mask_value, int k, int n_splits,
+                                 int64_t items_per_split, float *out_val, int64_t *out_idx,
+                                 float *part_val, int32_t *part_idx, hipStream_t stream) {
+#define LG_SCREEN_LAUNCH(NG, MM, W)                                                            \
+  {                                                                                           \
+    const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
+    const int64_t tiles = (n_users + upb - 1) / upb;                                          \
+    k_score_topk_screen<D, NG, MM, W><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, \
+                                        stream>>>(eu, ei, eub, eib, umarg, n_users, n_items,  \
+                                                  ex_rowptr, ex_col, mask_value, k, n_splits, \
+                                                  items_per_split, out_val, out_idx, part_val, \
+                                                  part_idx);                                  \
+  }
+  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 4)
+  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2)
+  else LG_SCREEN_LAUNCH(1, 4, 2)
+#undef LG_SCREEN_LAUNCH
+}
+
 static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
 
 static int64_t split_len(int64_t n_items, int n_splits) {
@@ -548,6 +798,60 @@ extern "C" int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_use
     k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
                                                         out_val, out_idx);
   return launch_status("lg_score_topk_f32(merge)");
+}
+
+extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, const void *eu_bf16,
+                                          const void *ei_bf16, const float *umarg,
+                                          int64_t n_users, int64_t n_items, int32_t dim,
+                                          const int64_t *ex_rowptr, const int32_t *ex_col,
+                                          float mask_value, int32_t k, int32_t n_splits,
+                                          float *out_val, int64_t *out_idx, void *ws,
+                                          size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && eu_bf16 && ei_bf16 && umarg && out_val && out_idx,
+             "lg_score_topk_screened_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items > 0 && n_items < 0x7fffffff,
+             "lg_score_topk_screened_f32: n_items must be in [1, 2^31-1)");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128,
+             "lg_score_topk_screened_f32: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_score_topk_screened_f32: k=%d not in [1,128]", k);
+  LG_REQUIRE(n_splits >= 1 && n_splits <= 4096, "lg_score_topk_screened_f32: bad n_splits %d",
+             n_splits);
+  LG_REQUIRE(!ex_rowptr == !ex_col,
+             "lg_score_topk_screened_f32: ex_rowptr/ex_col must both be set");
+  LG_REQUIRE(((uintptr_t)eu_bf16 & 15) == 0 && ((uintptr_t)ei_bf16 & 15) == 0,
+             "lg_score_topk_screened_f32: bf16 copies must be 16-byte aligned");
+  if (n_users == 0) return LG_OK;
+  const int64_t per = split_len(n_items, n_splits);
+  const int ns = (int)((n_items + per - 1) / per);
+  float *part_val = nullptr;
+  int32_t *part_idx = nullptr;
+  if (ns > 1) {
+    const size_t need = lg_score_topk_ws_bytes(n_users, n_items, dim, k, ns);
+    if (!ws || ws_bytes < need) {
+      set_error("lg_score_topk_screened_f32: workspace %zu < %zu bytes", ws_bytes, need);
+      return LG_ERR_WORKSPACE;
+    }
+    part_val = (float *)ws;
+    part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int M = cap_m(k);
+  const __bf16 *ub = (const __bf16 *)eu_bf16, *ib = (const __bf16 *)ei_bf16;
+  switch (dim) {
+    case 32: dispatch_topk_screen<32>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    case 64: dispatch_topk_screen<64>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    default: dispatch_topk_screen<128>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+  }
+  int st = launch_status("lg_score_topk_screened_f32");
+  if (st != LG_OK || ns == 1) return st;
+  const unsigned blocks = (unsigned)((n_users + 3) / 4);
+  if (k <= 64)
+    k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  else
+    k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  return launch_status("lg_score_topk_screened_f32(merge)");
 }
 
 extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_users,

@@ -59,6 +59,11 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _f32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],
     ),
+    "lg_score_topk_screened_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _f32, _i32, _i32, _vp, _vp, _vp,
+         _sz, _vp],
+    ),
     "lg_score_dense_f32": (
         ctypes.c_int,
         [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _f32, _vp, _i64, _vp],

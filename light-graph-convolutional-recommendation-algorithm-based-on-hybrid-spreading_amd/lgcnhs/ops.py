@@ -191,10 +191,22 @@ def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512) -> int:
     return best
 
 
+# |bf16 MFMA product - fp32 chain| <= 0.00785 ||u|| ||i|| (csrc/gbound.hip); 3 % slack for
+# the fp32 roundings of the margin and of the screen's compare
+SCREEN_MARGIN = 0.0081
+SCREEN_DEFAULT = False  # (set once the screened kernel is measured on the box)
+
+
 def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None = None,
-               mask_value: float = MASK_VALUE, n_splits: int | None = None):
+               mask_value: float = MASK_VALUE, n_splits: int | None = None,
+               screen: bool | None = None):
     """Top-k items per user by the masked e0 score; returns (values fp32 [U,k],
-    indices int64 [U,k]) sorted by (score desc, item asc)."""
+    indices int64 [U,k]) sorted by (score desc, item asc). screen=True runs
+    lg_score_topk_screened_f32: a bf16 MFMA bound decides which 16-item tiles get the exact
+    fp32 chain; the results are lg_score_topk_f32's (screen=False) bit for bit. Default:
+    SCREEN_DEFAULT."""
+    if screen is None:
+        screen = SCREEN_DEFAULT
     eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
     nu, d = eu.shape
     ni = ei.shape[0]
@@ -208,10 +220,21 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
     val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)
     idx = torch.empty((nu, k), dtype=torch.int64, device=eu.device)
+    ex_rp = N.ptr(excl.rowptr if excl else None)
+    ex_c = N.ptr(excl.col if excl else None)
+    if screen and nu > 0:
+        ub, un = bound_operands(eu)
+        ib, inorm = bound_operands(ei)
+        umarg = un * (inorm.max() * SCREEN_MARGIN)
+        N.check(N.lib().lg_score_topk_screened_f32(
+            N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d, ex_rp, ex_c,
+            float(mask_value), int(k), ns, N.ptr(val), N.ptr(idx), N.ptr(ws), ws_bytes,
+            N.stream_handle(eu.device)), "lg_score_topk_screened_f32")
+        return val, idx
     N.check(N.lib().lg_score_topk_f32(
-        N.ptr(eu), N.ptr(ei), nu, ni, d, N.ptr(excl.rowptr if excl else None),
-        N.ptr(excl.col if excl else None), float(mask_value), int(k), ns, N.ptr(val),
-        N.ptr(idx), N.ptr(ws), ws_bytes, N.stream_handle(eu.device)), "lg_score_topk_f32")
+        N.ptr(eu), N.ptr(ei), nu, ni, d, ex_rp, ex_c, float(mask_value), int(k), ns,
+        N.ptr(val), N.ptr(idx), N.ptr(ws), ws_bytes, N.stream_handle(eu.device)),
+        "lg_score_topk_f32")
     return val, idx
 
 

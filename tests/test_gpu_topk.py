@@ -52,18 +52,46 @@ def test_score_dense_masked(d):
     assert np.array_equal(G.view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("screen", [True, False])
 @pytest.mark.parametrize("d", [32, 64, 128])
 @pytest.mark.parametrize("k", [1, 5, 20, 32, 33, 64, 100, 128])
-def test_score_topk_bit_exact(d, k):
+def test_score_topk_bit_exact(d, k, screen):
+    """lg_score_topk_screened_f32 (bf16 screen, the default) and lg_score_topk_f32: both
+    bit-exact against the C chain oracle."""
     from lgcnhs import ops
     U, I = 301, 2047
     eu, ei = _emb(U, d, 10 + k), _emb(I, d, 20 + d)
     rp, col = _excl(U, I, 0.03, k)
     ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
     for ns in (1, None, 7):
-        v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), n_splits=ns)
+        v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), n_splits=ns,
+                              screen=screen)
         np.testing.assert_array_equal(i.cpu().numpy(), oi)
         assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
+def test_screened_topk_near_ties_and_wide_norms():
+    """The bf16 screen's margin under stress: items that differ below bf16 resolution (their
+    bf16 products tie, the fp32 chain orders them), scaled items and users over 1e-3..1e2,
+    a zero user row: the screened lists equal the plain kernel's and the oracle's bit for
+    bit."""
+    from lgcnhs import ops
+    U, I, d, k = 96, 5000, 64, 20
+    eu, ei = _emb(U, d, 31), _emb(I, d, 32)
+    base = ei[:40].clone()
+    for r in range(1, 8):  # 7 near-copies of 40 items, each off by a sub-bf16 perturbation
+        ei[40 * r:40 * r + 40] = base * (1 + r * 2.0 ** -14)
+    g = torch.Generator().manual_seed(33)
+    ei *= torch.exp(torch.randn(I, 1, generator=g) * 1.5)
+    eu *= torch.exp(torch.randn(U, 1, generator=g) * 1.5)
+    eu[5] = 0.0
+    rp, col = _excl(U, I, 0.01, 34)
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))
+    v0, i0 = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), screen=False)
+    assert torch.equal(i, i0) and torch.equal(v.view(torch.int32), v0.view(torch.int32))
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
 def test_score_topk_edge_cases():
