@@ -87,7 +87,7 @@ def test_screened_topk_near_ties_and_wide_norms():
     eu[5] = 0.0
     rp, col = _excl(U, I, 0.01, 34)
     ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
-    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), screen=True)
     v0, i0 = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), screen=False)
     assert torch.equal(i, i0) and torch.equal(v.view(torch.int32), v0.view(torch.int32))
     np.testing.assert_array_equal(i.cpu().numpy(), oi)
