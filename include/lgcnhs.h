@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 9
+#define LG_ABI_VERSION 10
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -319,8 +319,7 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
  * lg_score_chunk_bound's [n_users][n_chunks] bounds for this tile (n_chunks =
  * ceil(width / 64) <= 64) and optionally qb/qstride, its per-column 8-bit bounds: only
  * columns whose bound (gb * q / 255 with qb) times F can beat the K-th value get the exact
- * score chain; q_rb != 0 says qb came from lg_score_chunk_bound with rbeta (the walk's rb
- * folded into q: its screen is then the final test).
+ * score chain.
  * Exclusions (dropped): ex_rowptr/ex_col as in lg_rows_topk_f64 plus a per-row cursor
  * ex_cur[n_users] positioned at the walk's first item by lg_spread_tile_seek(ex_rowptr,
  * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
@@ -335,7 +334,7 @@ int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *
                                      const double *inv_cls, int32_t item_begin, int32_t tile,
                                      int32_t width, const float *eu, const float *ei,
                                      int32_t dim, const float *gb, int32_t n_chunks,
-                                     const uint8_t *qb, int32_t qstride, int32_t q_rb,
+                                     const uint8_t *qb, int32_t qstride,
                                      const int64_t *ex_rowptr, const int32_t *ex_col,
                                      int64_t *ex_cur, int32_t k, int32_t first,
                                      double *io_val, int64_t *io_idx, lg_stream_t stream);
@@ -351,13 +350,11 @@ int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
  * lg_bound_prep_f32 of the users' rows and of all items. dim in {32, 64, 128}. qb (optional,
  * [n_users][qstride] bytes, qstride >= width rounded up to 256): per column j,
  * q = ceil(255 (G_bf16 + margin) / gb) in [0, 255], so gb * q / 255 >= the chain score too
- * (csrc/gbound.hip). rbeta (optional, with qb: the walk's rb of all items): q also carries
- * the column's rb_j / rbmax_c (rbmax_c = the largest rb over the column's 64-column chunk),
- * so gb * q * rbmax_c / 255 >= the chain score times rb_j. */
+ * (csrc/gbound.hip). */
 int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
                          const void *i_bf16, const float *i_norm, int32_t dim,
                          int32_t item_begin, int32_t width, float *gb, uint8_t *qb,
-                         int32_t qstride, const double *rbeta, lg_stream_t stream);
+                         int32_t qstride, lg_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Recommendation-list metrics (reference metrics/accurate.py and

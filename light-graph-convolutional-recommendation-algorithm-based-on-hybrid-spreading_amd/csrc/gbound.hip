@@ -13,11 +13,8 @@
 // Per column (optional qb): q_j = ceil(255 (G_bf16_j + the same margin) / gb (1 + 2^-20)),
 // clamped to [0, 255], so gb * q_j / 255 >= G_chain_j as well (q_j = 0 when the bound is
 // <= 0; gb <= 0 makes every column's bound <= 0). Stored row-major, one byte per column,
-// rows of qstride bytes. With rbeta (the walk's per-item HybridS factor rb = 1 / k_j^lambda)
-// the column's share of its chunk's largest rb is folded in as well:
-// q_j = ceil(255 (G_bf16_j + margin) (rb_j / rbmax_c) / gb (1 + 2^-20)^3), so
-// gb * q_j * rbmax_c / 255 >= G_chain_j * rb_j -- the walk's screen then needs no per-column
-// rb of its own (rbmax_c = the largest rb over the chunk's columns, exact, as the walk's).
+// rows of qstride bytes. (Folding the walk's rb_j / rbmax_c into q as well made the walk no
+// faster -- 2.68 vs 2.67 s over the 489 C5 tiles -- and the bounds 0.34 s slower: dropped.)
 // Then fl(G_chain * F) <= fl(gb * F) for every F >= 0 (rounding is monotone), so a column
 // with gb * F <= tau can not beat tau. Cost per tile: 2 * U * T * D flop on bf16 MFMA
 // (v_mfma_f32_16x16x32_bf16: 16 items x 16 users x 32 dims per instruction; 64 users per
@@ -77,8 +74,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
                                                      const float *__restrict__ inorm,
                                                      int32_t item_begin, int32_t width,
                                                      int32_t nch, float *__restrict__ gb,
-                                                     uint8_t *__restrict__ qb, int32_t qstride,
-                                                     const double *__restrict__ rbeta) {
+                                                     uint8_t *__restrict__ qb, int32_t qstride) {
   constexpr int S = D / 32;  // k-steps
   const int lane = lane_id();
   const int64_t ubase = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 64;
@@ -137,24 +133,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     float inm = na;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) inm = fmaxf(inm, __shfl_xor(inm, o));
-    // with rbeta: each of the lane's 16 columns' rb_j / rbmax_c, rounded up to fp32
-    float rr[4][4];
-    if (qb && rbeta) {
-      double rm = cb + lane < width ? rbeta[item_begin + cb + lane] : 0.0;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) rm = fmax(rm, __shfl_xor(rm, o));
-      const double inv_rm = rm > 0.0 ? 1.0 / rm : 0.0;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = cb + 16 * t + 4 * kg + r;
-          const double rt = j < width ? rbeta[item_begin + j] * inv_rm : 0.0;
-          // (the fp64 product is within 2 ulp of rb_j / rbmax_c; the fp32 rounding and
-          // those ulps are covered by the 2^-20 factor)
-          rr[t][r] = (float)rt * (1.f + 0x1p-20f);
-        }
-    }
     float gmax[4];
     f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
@@ -210,10 +188,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
           const f32x2 lo = __builtin_elementwise_fma(f32x2{accs[t][g][0], accs[t][g][1]}, sc2, ms2);
           const f32x2 hi = __builtin_elementwise_fma(f32x2{accs[t][g][2], accs[t][g][3]}, sc2, ms2);
           float v[4] = {lo[0], lo[1], hi[0], hi[1]};
-          if (rbeta) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = v[r] * rr[t][r] * (1.f + 0x1p-20f);
-          }
           uint32_t w = 0;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -272,7 +246,7 @@ extern "C" int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, vo
 extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
                                     const void *i_bf16, const float *i_norm, int32_t dim,
                                     int32_t item_begin, int32_t width, float *gb, uint8_t *qb,
-                                    int32_t qstride, const double *rbeta, lg_stream_t stream) {
+                                    int32_t qstride, lg_stream_t stream) {
   LG_REQUIRE(u_bf16 && u_norm && i_bf16 && i_norm && gb && n_users >= 0 && item_begin >= 0 &&
                  width >= 1,
              "lg_score_chunk_bound: bad arguments");
@@ -286,9 +260,9 @@ extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int
   hipStream_t s = (hipStream_t)stream;
   const __bf16 *u = (const __bf16 *)u_bf16, *i = (const __bf16 *)i_bf16;
   switch (dim) {
-    case 32: k_chunk_bound<32, 3><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride, rbeta); break;
-    case 64: k_chunk_bound<64, 3><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride, rbeta); break;
-    default: k_chunk_bound<128, 2><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride, rbeta); break;
+    case 32: k_chunk_bound<32, 3><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
+    case 64: k_chunk_bound<64, 3><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
+    default: k_chunk_bound<128, 2><<<grid, 256, 0, s>>>(u, u_norm, n_users, i, i_norm, item_begin, width, nch, gb, qb, qstride); break;
   }
   return launch_status("lg_score_chunk_bound");
 }

@@ -1038,7 +1038,6 @@ struct WalkArgs {
   int32_t nch;
   const uint8_t *qb;          // [n_users][qstride] per-column 8-bit bounds (or NULL)
   int32_t qstride;
-  int32_t q_rb;               // qb has rb_j / rbmax_c folded in (lg_score_chunk_bound rbeta)
   const int64_t *ex_rowptr;   // exclusions (dropped), with a per-row cursor
   const int32_t *ex_col;
   int64_t *ex_cur;
@@ -1568,8 +1567,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
             const uint32_t qq = t < 4 ? qa : qb2;
             const double bq = (double)((qq >> (8 * (t & 3))) & 0xFFu) *
                               __shfl(bq_v, (j >> 6) & 63);
-            // (q with rb folded in: the pre-screen was already this test)
-            const bool cand = has && (a.q_rb || bq * f > tau);
+            const bool cand = has && bq * f > tau;
             const uint64_t bal = __ballot(cand);
             if (bal) {
               const int nb = __popcll(bal);
@@ -2083,7 +2081,7 @@ extern "C" int lg_spread_tile_resource_topk_f64(
     int64_t n_users, const void *lines, const void *ovf, int32_t null_row, const double *rbeta,
     const double *inv_cls, int32_t item_begin, int32_t tile, int32_t width, const float *eu,
     const float *ei, int32_t dim, const float *gb, int32_t n_chunks, const uint8_t *qb,
-    int32_t qstride, int32_t q_rb, const int64_t *ex_rowptr,
+    int32_t qstride, const int64_t *ex_rowptr,
     const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
     int64_t *io_idx, lg_stream_t stream) {
   LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls &&
@@ -2128,7 +2126,6 @@ extern "C" int lg_spread_tile_resource_topk_f64(
   a.nch = n_chunks;
   a.qb = qb;
   a.qstride = qstride;
-  a.q_rb = qb ? q_rb : 0;
   a.ex_rowptr = ex_rowptr;
   a.ex_col = ex_col;
   a.ex_cur = ex_cur;

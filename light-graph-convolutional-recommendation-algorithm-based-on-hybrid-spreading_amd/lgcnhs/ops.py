@@ -194,7 +194,7 @@ def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512) -> int:
 # |bf16 MFMA product - fp32 chain| <= 0.00785 ||u|| ||i|| (csrc/gbound.hip); 3 % slack for
 # the fp32 roundings of the margin and of the screen's compare
 SCREEN_MARGIN = 0.0081
-SCREEN_DEFAULT = False  # (set once the screened kernel is measured on the box)
+SCREEN_DEFAULT = True  # measured: 26.8 vs 31.9 ms (d=64), 45.8 vs 59.7 ms (d=128) at C5
 
 
 def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None = None,
@@ -645,7 +645,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
                       ei: torch.Tensor | None = None, users: slice | None = None,
                       tile: int = 2048, items: slice | None = None,
                       stats: dict | None = None, count_paths: bool = False,
-                      col_bounds: bool = True, rb_in_bounds: bool = False, **_):
+                      col_bounds: bool = True, **_):
     """Per-user top-k of (G *) F, F = A @ HybridS(A, general_W, lam), over item tiles:
     never holds general_W, W (I x I) or F (U x I). The values of spread_topk(A,
     hybrid_weight(spread_general(A), A.k_item, lam), ...) within a few ulp (the walk's
@@ -684,8 +684,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
     eu_r = None if eu is None else eu[u0:u1]
     if stats is not None and count_paths:
         _count_rows(tw, A, u0, u1)
-    walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile, col_bounds,
-                    rb_in_bounds)
+    walk = TileWalk(A, u0, u1, i0, k, ex if drop else None, eu_r, ei, tile, col_bounds)
     evs = [] if stats is not None else None
     for j0 in range(i0, i1, tile):
         if evs is not None:  # per-tile HIP events on the launch stream: build / bounds / walk
@@ -769,12 +768,11 @@ def bound_operands(x: torch.Tensor):
 
 
 def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
-                 out: torch.Tensor | None = None, qout: torch.Tensor | None = None,
-                 rbeta: torch.Tensor | None = None):
+                 out: torch.Tensor | None = None, qout: torch.Tensor | None = None):
     """[users, ceil(width/64)] fp32 upper bounds of the fp32 score chain over each 64-column
     chunk of items [j0, j0 + width) (lg_score_chunk_bound); with qout ([users, qstride]
-    uint8, qstride >= width rounded up to 256) also the per-column 8-bit bounds, with rbeta
-    (fp64 rb of all items) those carrying rb_j / rbmax_c. Returns gb, or (gb, q) with qout."""
+    uint8, qstride >= width rounded up to 256) also the per-column 8-bit bounds. Returns gb,
+    or (gb, q) with qout."""
     n = ub.shape[0]
     nch = -(-width // 64)
     if out is None or out.numel() < n * nch:
@@ -784,7 +782,6 @@ def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
     N.check(N.lib().lg_score_chunk_bound(N.ptr(ub), N.ptr(un), n, N.ptr(ib), N.ptr(inorm),
                                          int(dim), int(j0), int(width), N.ptr(gb),
                                          N.ptr(qout), int(qs),
-                                         N.ptr(rbeta if qout is not None else None),
                                          N.stream_handle(ub.device)),
             "lg_score_chunk_bound")
     return gb if qout is None else (gb, qout)
@@ -799,9 +796,8 @@ class TileWalk:
 
     def __init__(self, A: Interactions, u0: int, u1: int, i0: int, k: int,
                  ex: RowSets | None, eu=None, ei=None, tile: int = 2048,
-                 col_bounds: bool = True, rb_in_bounds: bool = False):
+                 col_bounds: bool = True):
         self.A, self.u0, self.u1, self.i0, self.k, self.ex = A, u0, u1, i0, int(k), ex
-        self.rb_in_bounds = bool(rb_in_bounds and col_bounds)
         self.n = u1 - u0
         self.dev = A.k_item.device
         self.vals = torch.full((self.n, self.k), float("-inf"), dtype=torch.float64,
@@ -837,18 +833,14 @@ class TileWalk:
                     "lg_spread_tile_seek")
 
     def bounds(self, j0: int, width: int, scale: "HybridScale | None" = None):
-        """(gb, q) score bounds of tile [j0, j0 + width) (q None: chunk bounds only); with
-        rb_in_bounds, q carries the columns' rb (scale.rb) relative to their chunk's."""
+        """(gb, q) score bounds of tile [j0, j0 + width) (q None: chunk bounds only)."""
         if not self.d:
             return None
         if self.qbuf is None:
             return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
                                 self.gbuf), None
-        rb = scale.rb if (self.rb_in_bounds and scale is not None) else None
-        if self.rb_in_bounds and rb is None:
-            raise ValueError("rb_in_bounds needs the walk's HybridScale")
         return chunk_bounds(self.ub, self.un, self.ib, self.inorm, self.d, j0, width,
-                            self.gbuf, self.qbuf, rb)
+                            self.gbuf, self.qbuf)
 
     def step(self, lines, ovf, inv_cls, scale: HybridScale, j0: int, tile: int, width: int,
              first: bool, bnd=None) -> None:
@@ -863,7 +855,7 @@ class TileWalk:
             N.ptr(A.by_user.rowptr[self.u0:]), N.ptr(A.by_user.col), N.ptr(scale.ra_edge),
             self.n, N.ptr(lines), N.ptr(ovf), A.n_items, N.ptr(scale.rb), N.ptr(inv_cls), int(j0),
             int(tile), int(width), N.ptr(self.eu), N.ptr(self.ei), self.d, N.ptr(gb), nch,
-            N.ptr(q), 0 if q is None else q.shape[1], int(self.rb_in_bounds and q is not None),
+            N.ptr(q), 0 if q is None else q.shape[1],
             N.ptr(ex.rowptr if ex is not None else None),
             N.ptr(ex.col if ex is not None else None), N.ptr(self.ex_cur), self.k,
             int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), N.stream_handle(self.dev)),

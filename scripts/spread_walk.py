@@ -22,8 +22,8 @@ ap.add_argument("--no-g", action="store_true", help="no G factor (SpreadMethod)"
 ap.add_argument("--count", action="store_true", help="count paths / row bytes (extra work)")
 ap.add_argument("--no-col-bounds", action="store_true",
                 help="chunk score bounds only (no per-column 8-bit bounds)")
-ap.add_argument("--rb-in-bounds", action="store_true",
-                help="per-column bounds carry rb_j / rbmax_c (lg_score_chunk_bound rbeta)")
+ap.add_argument("--no-excl", action="store_true",
+                help="no exclusion sets (timing of the walk without the per-user exclusion cursor)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
@@ -33,13 +33,12 @@ del keys
 g = torch.Generator(device=dev).manual_seed(42)
 eu = torch.randn(U, D, device=dev, generator=g) * 0.1
 ei = torch.randn(I, D, device=dev, generator=g) * 0.1
-kw = {} if a.no_g else {"eu": eu, "ei": ei, "col_bounds": not a.no_col_bounds,
-                        "rb_in_bounds": a.rb_in_bounds}
+kw = {} if a.no_g else {"eu": eu, "ei": ei, "col_bounds": not a.no_col_bounds}
 for rep in range(a.reps):
     torch.cuda.synchronize()
     t = time.time()
     st = {}
-    vals, idxs = ops.spread_topk_tiled(A, 0.5, 20, A.by_user, tile=a.tile,
+    vals, idxs = ops.spread_topk_tiled(A, 0.5, 20, None if a.no_excl else A.by_user, tile=a.tile,
                           items=slice(0, a.tiles * a.tile),
                           stats=st if rep == 0 else None, count_paths=a.count, **kw)
     torch.cuda.synchronize()

@@ -441,55 +441,3 @@ def test_score_bounds_cover_chain_scores(d):
     assert not bad.any(), (np.argwhere(bad)[:5], colb[bad][:5], G[bad][:5])
     # and tight: the column bound is within a few % of the chunk bound's scale of the score
     assert np.mean(colb - G) < np.mean(gbn[:, chunk] - G)
-
-
-@pytest.mark.parametrize("d", [32, 64, 128])
-def test_score_bounds_with_rb_cover_chain_scores_times_rb(d):
-    """lg_score_chunk_bound with rbeta: gb * q * rbmax_c / 255 >= the fp32 chain score times
-    rb_j for every column (rbmax_c = the largest rb of the column's 64-column chunk), and
-    q never exceeds the plain bound's (rb_j <= rbmax_c)."""
-    from lgcnhs import ops
-    from oracle import lgcn_oracle as O
-    g = torch.Generator().manual_seed(10 + d)
-    U, W, j0 = 70, 333, 40
-    eu = torch.randn(U, d, generator=g) * 0.1
-    ei = torch.randn(j0 + W + 5, d, generator=g) * 0.1
-    eu[3] *= 40.0
-    k_item = torch.randint(1, 500, (j0 + W + 5,), generator=g).double()
-    rb = 1.0 / k_item.pow(0.37)
-    ub, un = ops.bound_operands(eu.to(DEV))
-    ib, inn = ops.bound_operands(ei.to(DEV))
-    qs = -(-W // 256) * 256
-    q0 = torch.zeros((U, qs), dtype=torch.uint8, device=DEV)
-    q1 = torch.zeros((U, qs), dtype=torch.uint8, device=DEV)
-    gb0, q0 = ops.chunk_bounds(ub, un, ib, inn, d, j0, W, qout=q0)
-    gb0 = gb0.clone()
-    gb1, q1 = ops.chunk_bounds(ub, un, ib, inn, d, j0, W, qout=q1, rbeta=rb.to(DEV))
-    assert torch.equal(gb0, gb1)
-    G = O.chain_scores(eu.numpy(), ei[j0:j0 + W].numpy()).astype(np.float64)
-    rbn = rb.numpy()[j0:j0 + W]
-    chunk = np.arange(W) // 64
-    rbmax = np.array([rbn[64 * c:64 * c + 64].max() for c in range(chunk.max() + 1)])
-    gbn = gb1.cpu().numpy().astype(np.float64)
-    qn = q1.cpu().numpy()[:, :W].astype(np.float64)
-    colb = gbn[:, chunk] * qn / 255.0 * rbmax[chunk]
-    bad = colb < G * rbn
-    assert not bad.any(), (np.argwhere(bad)[:5], colb[bad][:5], (G * rbn)[bad][:5])
-    assert (q1.cpu().numpy()[:, :W] <= q0.cpu().numpy()[:, :W]).all()
-
-
-def test_rb_in_bounds_walk_lists_bitwise():
-    """The walk screened with rb folded into the column bounds returns the lists of the
-    plain screen bit for bit (same exact scores, same insertions)."""
-    from lgcnhs import ops
-    U, I, d = 400, 1500, 64
-    A = _inter(U, I, 14000, seed=21, zipf=True)
-    g = torch.Generator(device=DEV).manual_seed(4)
-    eu = torch.randn(U, d, device=DEV, generator=g) * 0.1
-    ei = torch.randn(I, d, device=DEV, generator=g) * 0.1
-    for lam in (0.2, 0.5, 0.9):
-        v0, i0 = ops.spread_topk_tiled(A, lam, 20, A.by_user, eu=eu, ei=ei, tile=512)
-        v1, i1 = ops.spread_topk_tiled(A, lam, 20, A.by_user, eu=eu, ei=ei, tile=512,
-                                       rb_in_bounds=True)
-        assert torch.equal(i0, i1)
-        assert torch.equal(v0.view(torch.int64), v1.view(torch.int64))
