@@ -324,7 +324,9 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
  * ex_cur[n_users] positioned at the walk's first item by lg_spread_tile_seek(ex_rowptr,
  * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
  * lg_rows_topk_f64 over the F rows the walk sums. k in [1, 128]; dim in
- * {32, 64, 128}. lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
+ * {32, 64, 128}. The walk keeps its stream positions in 32 bits: n_users, the interactions
+ * (user_rowptr[n_users]) and the exclusions (ex_rowptr[n_users]) must each be < 2^31.
+ * lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
  * workgroup's tables (the launch fits as many waves per CU as the LDS holds). */
 size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
 int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *user_items,

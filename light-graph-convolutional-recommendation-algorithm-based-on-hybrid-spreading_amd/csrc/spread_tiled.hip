@@ -1013,9 +1013,10 @@ constexpr int kBatchRows = 8 * kWalkQ;
 // at least 64 entries whatever the batch size
 constexpr int kOvfList = kBatchRows > 64 ? kBatchRows : 64;
 constexpr int kDecodePhase = 4;  // lines whose class reads precede their adds
-// q dwords per lane loaded with the user's first batch (256 columns each), then streamed
-// kQPre / 2 scan iterations ahead (4 and 8 measured no faster than 2: 3.22 / 3.33 vs 3.20 s)
-constexpr int kQPre = 2;
+// q dwords per lane loaded with the user's state (256 columns each: a whole 2048-column
+// tile); the columns of wider tiles past them are screened by their chunk bound alone (q =
+// 255), so the scan issues no memory loads
+constexpr int kQPre = 8;
 static_assert(kWalkQ % kDecodePhase == 0, "decode phase must divide the batch's line loads");
 
 struct WalkArgs {
@@ -1123,10 +1124,27 @@ __device__ __forceinline__ void add_slot_fast(double *acc, uint32_t s, double ra
   if (s) lds_add(acc, s & 0xFFFFu, inv * ra);
 }
 
-// A batch of the wave's stream: rows [r0, r1) of user u (whose rows end at e).
+// A batch of the wave's stream: rows [r0, r1) of user u (whose rows end at e); xc / xh =
+// the user's exclusion cursor and row end (prefetched with its row pointers). 32-bit fields
+// (the host requires users, interactions and exclusions < 2^31): the stream state then fits
+// the SGPRs without spilling into VGPR lanes.
 struct Batch {
-  int64_t u, r0, r1, e;
+  int32_t u, r0, r1, e;
   bool first;
+  int32_t xc, xh;
+};
+
+// The top-K state of a batch's user, loaded with the batch's lines (every batch loads it:
+// the loads are unconditional, so the compiler's vmcnt bookkeeping never waits for a
+// younger load than the one it needs): the running list (lane, 64 + lane), the chunk score
+// bound, the per-column 8-bit bounds of the first kQPre * 256 columns and the next 64
+// excluded items.
+struct UState {
+  int lid0, lid1;
+  double lv0, lv1;
+  float gb;
+  uint32_t q[kQPre];
+  int32_t xw;
 };
 
 template <int MODE, int D, int M>
@@ -1187,23 +1205,38 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   const int64_t u_first = (int64_t)blockIdx.x * nw + wave;
   if (u_first >= n_users) return;
 
-  // row pointers of the next new user of the stream (prefetched one user ahead)
-  int64_t uq = u_first, bq = a.user_rowptr[u_first], eq = a.user_rowptr[u_first + 1];
+  // row pointers (and exclusion cursor) of the next new user of the stream, prefetched one
+  // user ahead
+  const bool has_ex = MODE == MODE_TOPK && a.ex_rowptr != nullptr;
+  int32_t uq = (int32_t)u_first, bq = (int32_t)a.user_rowptr[u_first],
+          eq = (int32_t)a.user_rowptr[u_first + 1];
+  int32_t xcq = 0, xhq = 0;
+  if (has_ex) {
+    xcq = (int32_t)a.ex_cur[u_first];
+    xhq = (int32_t)a.ex_rowptr[u_first + 1];
+  }
   auto new_user = [&]() __attribute__((always_inline)) {
-    Batch y{uq, bq, bq + kBatchRows < eq ? bq + kBatchRows : eq, eq, true};
-    uq += G;
+    Batch y{uq, bq, bq + kBatchRows < eq ? bq + kBatchRows : eq, eq, true, xcq, xhq};
+    uq += (int32_t)G;
     if (uq < n_users) {
-      bq = a.user_rowptr[uq];
-      eq = a.user_rowptr[uq + 1];
+      bq = (int32_t)a.user_rowptr[uq];
+      eq = (int32_t)a.user_rowptr[uq + 1];
+      if (has_ex) {
+        xcq = (int32_t)a.ex_cur[uq];
+        xhq = (int32_t)a.ex_rowptr[uq + 1];
+      }
     }
     return y;
   };
+  const Batch kEnd{(int32_t)n_users, 0, 0, 0, false, 0, 0};  // past the end of the stream
   auto next_batch = [&](const Batch &x) __attribute__((always_inline)) {
+    if (x.u >= n_users) return kEnd;
     if (x.r1 < x.e) {
-      Batch y{x.u, x.r1, x.r1 + kBatchRows < x.e ? x.r1 + kBatchRows : x.e, x.e, false};
+      Batch y{x.u, x.r1, x.r1 + kBatchRows < x.e ? x.r1 + kBatchRows : x.e, x.e, false, x.xc,
+              x.xh};
       return y;
     }
-    if (x.u + G >= n_users) return Batch{n_users, 0, 0, 0, false};  // end of the stream
+    if (x.u + G >= n_users) return kEnd;
     return new_user();
   };
   // item ids of a batch's rows (lanes of one 8-lane group: one row)
@@ -1213,7 +1246,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   const __amdgpu_buffer_rsrc_t r_lines = __builtin_amdgcn_make_buffer_rsrc(
       (void *)a.lines, 0, (int)((uint32_t)(a.null_row + 1) * 128u), 0x00020000);
   auto load_ids = [&](const Batch &x, int32_t (&it)[Q]) __attribute__((always_inline)) {
-    if (x.r1 > x.r0) {
+    {  // (unconditional: an empty batch reads 0 through a 0-byte descriptor)
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void *)(a.user_items + x.r0), 0, (int)((x.r1 - x.r0) * 4), 0x00020000);
 #pragma unroll
@@ -1241,51 +1274,39 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     }
   };
 
-  // ---- top-K state of the current user (MODE_TOPK), loaded at its first batch
+  // ---- top-K state of a batch's user (MODE_TOPK), loaded with the batch's lines: every load
+  // is issued (clamped user, 0-byte descriptors for absent operands), the consumers apply the
+  // masks at the finish
   constexpr bool kTwo = M > 2;  // k > 64: the list spans two registers per lane
-  int lid0 = -1, lid1 = -1;
-  double lv0 = 0.0, lv1 = 0.0;
-  float gbv = 0.f;
-  // the per-column bounds of the user's first kQPre * 256 columns (dword k: columns
-  // 256 k + 4 lane .. + 3), loaded with the user's first batch so the scan never waits
-  uint32_t qr[kQPre];
-#pragma unroll
-  for (int k = 0; k < kQPre; ++k) qr[k] = 0xFFFFFFFFu;
-  int64_t xpos = 0, xhi = 0;
-  int32_t xw = 0x7fffffff;
-  auto load_user = [&](int64_t u) __attribute__((always_inline)) {
+  const bool has_qb = MODE == MODE_TOPK && D > 0 && a.qb != nullptr;
+  auto load_state = [&](const Batch &x, UState &st) __attribute__((always_inline)) {
     if constexpr (MODE == MODE_TOPK) {
       const int k = a.k;
-      lid0 = lid1 = -1;
-      if (!a.first) {
-        // ids < 2^31 (and -1): the low dword of the int64 entry
-        const int *idx32 = reinterpret_cast<const int *>(a.io_idx);
-        const int e0 = lane < k ? lane : k - 1;
-        lid0 = idx32[2 * (u * k + e0)];
-        lv0 = a.io_val[u * k + e0];
-        if (lane >= k) lid0 = -1;
-        if constexpr (kTwo) {
-          const int e1 = 64 + lane < k ? 64 + lane : k - 1;
-          lid1 = idx32[2 * (u * k + e1)];
-          lv1 = a.io_val[u * k + e1];
-          if (64 + lane >= k) lid1 = -1;
-        }
+      const int64_t us = x.u < n_users ? x.u : n_users - 1;
+      // ids < 2^31 (and -1): the low dword of the int64 entry
+      const int *idx32 = reinterpret_cast<const int *>(a.io_idx);
+      const int e0 = lane < k ? lane : k - 1;
+      st.lid0 = idx32[2 * (us * k + e0)];
+      st.lv0 = a.io_val[us * k + e0];
+      if constexpr (kTwo) {
+        const int e1 = 64 + lane < k ? 64 + lane : k - 1;
+        st.lid1 = idx32[2 * (us * k + e1)];
+        st.lv1 = a.io_val[us * k + e1];
       }
       if constexpr (D > 0) {
-        gbv = a.gb[u * a.nch + (lane < a.nch ? lane : 0)];
-        if (a.qb) {
+        st.gb = a.gb[us * a.nch + (lane < a.nch ? lane : 0)];
+        const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+            has_qb ? (void *)(a.qb + us * a.qstride) : (void *)a.lines, 0,
+            has_qb ? a.qstride : 0, 0x00020000);
 #pragma unroll
-          for (int k = 0; k < kQPre; ++k)
-            if (256 * k < a.qstride)
-              qr[k] = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + 256 * k + 4 * lane);
-        }
+        for (int kk = 0; kk < kQPre; ++kk)
+          st.q[kk] = __builtin_amdgcn_raw_buffer_load_b32(rq, (uint32_t)(4 * lane), 256 * kk, 0);
       }
-      if (a.ex_rowptr) {
-        xpos = a.ex_cur[u];
-        xhi = a.ex_rowptr[u + 1];
-        xw = 0x7fffffff;
-        if (xpos + lane < xhi) xw = a.ex_col[xpos + lane];
-      }
+      const int32_t nx = x.xh - x.xc;
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          has_ex ? (void *)(a.ex_col + x.xc) : (void *)a.lines, 0,
+          has_ex ? (int)(4 * (nx < 64 ? nx : 64)) : 0, 0x00020000);
+      st.xw = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rx, (uint32_t)(4 * lane), 0, 0);
     }
   };
 
@@ -1301,12 +1322,17 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       // The LDS serves a wave's operations in order, so a class-table read issued after an
       // atomic returns only once the atomic is done: the reads of H lines' slots go out
       // first, then their adds (one wait per phase, not one per slot).
+      // (line groups wholly past a short batch's rows hold the zero line: their reads and
+      // adds are skipped with a wave-uniform branch; their loads were issued regardless)
       constexpr int H = kDecodePhase;
+      const int nr = (int)(x.r1 - x.r0);
 #pragma unroll
       for (int q0 = 0; q0 < Q; q0 += H) {
+        if (8 * q0 >= nr) break;
         double inv[H][4];
 #pragma unroll
         for (int q = 0; q < H; ++q) {
+          if (8 * (q0 + q) >= nr) break;
           inv[q][0] = slot_inv_fast(w[q0 + q].x & hmask);
           inv[q][1] = slot_inv_fast(w[q0 + q].y);
           inv[q][2] = slot_inv_fast(w[q0 + q].z);
@@ -1314,6 +1340,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         }
 #pragma unroll
         for (int q = 0; q < H; ++q) {
+          if (8 * (q0 + q) >= nr) break;
           const uint32_t sv[4] = {w[q0 + q].x & hmask, w[q0 + q].y, w[q0 + q].z, w[q0 + q].w};
 #pragma unroll
           for (int t = 0; t < 4; ++t)
@@ -1367,7 +1394,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   };
 
   // ---- the user's tile of F: written out (MODE_F) or merged into its top-K list
-  auto finish_user = [&](int64_t u) __attribute__((always_inline)) {
+  auto finish_user = [&](const Batch &x, UState &st) __attribute__((always_inline)) {
+    const int64_t u = x.u;
     wave_sync();
     if constexpr (MODE == MODE_F) {
       double *row = a.F + u * a.ldf;
@@ -1378,11 +1406,26 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     } else {
       const int k = a.k;
       // the running list in registers: entry lane (L0, I0) and 64 + lane (L1, I1), sorted by
-      // (value desc, id asc); empty entries (-inf, kPadId)
-      double L0 = lid0 >= 0 ? lv0 : neg_inf<double>();
-      double L1 = kTwo && lid1 >= 0 ? lv1 : neg_inf<double>();
-      int I0 = lid0 >= 0 ? lid0 : kPadId;
-      int I1 = kTwo && lid1 >= 0 ? lid1 : kPadId;
+      // (value desc, id asc); empty entries (-inf, kPadId); a first tile starts empty
+      const bool ok0 = !a.first && lane < k && st.lid0 >= 0;
+      double L0 = ok0 ? st.lv0 : neg_inf<double>();
+      int I0 = ok0 ? st.lid0 : kPadId;
+      double L1 = neg_inf<double>();
+      int I1 = kPadId;
+      if constexpr (kTwo) {
+        const bool ok1 = !a.first && 64 + lane < k && st.lid1 >= 0;
+        L1 = ok1 ? st.lv1 : neg_inf<double>();
+        I1 = ok1 ? st.lid1 : kPadId;
+      }
+      const float gbv = st.gb;
+      uint32_t (&qr)[kQPre] = st.q;
+      if (!has_qb) {
+#pragma unroll
+        for (int kk = 0; kk < kQPre; ++kk) qr[kk] = 0xFFFFFFFFu;
+      }
+      int64_t xpos = x.xc;
+      const int64_t xhi = x.xh;
+      int32_t xw = has_ex && xpos + lane < xhi ? st.xw : 0x7fffffff;
       auto kth = [&](double &tv, int &ti) __attribute__((always_inline)) {
         if (!kTwo || k <= 64) {
           tv = __shfl(L0, k - 1);
@@ -1423,7 +1466,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       };
       // excluded items of this tile (the next run of the user's sorted exclusion row): -1
       const int32_t lim = a.item_begin + a.width;
-      if (a.ex_rowptr) {
+      if (has_ex) {
         for (;;) {
           const bool in = xw < lim;
           if (in && xw >= a.item_begin) acc[xw - a.item_begin] = neg_inf<double>();
@@ -1502,21 +1545,13 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         sc_v = s_rbc[lane < a.nch ? lane : 0] * (1.0 + 0x1p-50) * gp * (1.0 / 255.0);
         bq_v = gp * (1.0 / 255.0) * (1.0 + 0x1p-50);
       }
-      auto q_at = [&](int c0) __attribute__((always_inline)) {  // q dword of column c0 + 4l
-        uint32_t q = 0xFFFFFFFFu;
-        if constexpr (D > 0)
-          if (a.qb && c0 < a.qstride)
-            q = *reinterpret_cast<const uint32_t *>(a.qb + u * a.qstride + c0 + 4 * lane);
-        return q;
-      };
       const double2 zero2{0.0, 0.0};
       for (int c0 = 0; c0 < a.width; c0 += 512) {
         const uint32_t qa = qr[0], qb2 = qr[1];
 #pragma unroll
         for (int k = 0; k + 2 < kQPre; ++k) qr[k] = qr[k + 2];
-        // wider tiles: the bounds kQPre / 2 iterations ahead
-        qr[kQPre - 2] = q_at(c0 + 256 * kQPre);
-        qr[kQPre - 1] = q_at(c0 + 256 * kQPre + 256);
+        qr[kQPre - 2] = 0xFFFFFFFFu;  // (columns past 256 kQPre: the chunk bound alone)
+        qr[kQPre - 1] = 0xFFFFFFFFu;
         double sv[8];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
@@ -1607,36 +1642,51 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   };
 
   // ---- the pipeline: c (decoded now; lines in wc), d (lines in flight in wd), n2 (ids in
-  // flight in it2). Two register sets alternate between c and d.
+  // flight in it2). Two register sets (lines, ra, user state) alternate between c and d. Every
+  // step issues the same loads (empty batches read the zero line / 0 bytes), so the wait
+  // before a decode counts the two younger batches' loads instead of draining them.
   int32_t it2[Q];
   uint4 w0[Q], w1[Q];
   double ra0[Q], ra1[Q];
+  UState s0, s1;
   Batch c = new_user();
   load_ids(c, it2);
   load_rows(c, it2, w0, ra0);
+  load_state(c, s0);
   Batch d = next_batch(c);
-  if (d.u < n_users) {
-    load_ids(d, it2);
-    load_rows(d, it2, w1, ra1);
-  }
-  Batch n2 = d.u < n_users ? next_batch(d) : Batch{n_users, 0, 0, 0, false};
-  if (n2.u < n_users) load_ids(n2, it2);
-  auto step = [&](uint4 (&wc)[Q], double (&rc)[Q]) __attribute__((always_inline)) {
-    if (c.first) load_user(c.u);
+  load_ids(d, it2);
+  load_rows(d, it2, w1, ra1);
+  load_state(d, s1);
+  Batch n2 = next_batch(d);
+  load_ids(n2, it2);
+  auto step = [&](uint4 (&wc)[Q], double (&rc)[Q], UState &sc) __attribute__((always_inline)) {
+    // c's user state (loaded two steps ago) is taken here, where the wait for it counts the
+    // younger batches' loads; at the finish, behind the exclusion loop's load, the compiler
+    // would drain every load in flight
+    if constexpr (MODE == MODE_TOPK) {
+      asm volatile("" : "+v"(sc.lid0), "+v"(sc.lv0), "+v"(sc.xw));
+      if constexpr (kTwo) asm volatile("" : "+v"(sc.lid1), "+v"(sc.lv1));
+      if constexpr (D > 0) {
+        asm volatile("" : "+v"(sc.gb));
+#pragma unroll
+        for (int kk = 0; kk < kQPre; ++kk) asm volatile("" : "+v"(sc.q[kk]));
+      }
+    }
     decode(c, wc, rc);
-    if (c.r1 >= c.e) finish_user(c.u);
+    if (c.r1 >= c.e) finish_user(c, sc);
     // batch t+2 into the freed registers (issued before the scan instead: 1.5 % slower)
-    if (n2.u < n_users) load_rows(n2, it2, wc, rc);
-    const Batch n3 = n2.u < n_users ? next_batch(n2) : Batch{n_users, 0, 0, 0, false};
-    if (n3.u < n_users) load_ids(n3, it2);
+    load_rows(n2, it2, wc, rc);
+    load_state(n2, sc);
+    const Batch n3 = next_batch(n2);
+    load_ids(n3, it2);
     c = d;
     d = n2;
     n2 = n3;
     return c.u < n_users;
   };
   for (;;) {
-    if (!step(w0, ra0)) break;
-    if (!step(w1, ra1)) break;
+    if (!step(w0, ra0, s0)) break;
+    if (!step(w1, ra1, s1)) break;
   }
 }
 
@@ -2085,7 +2135,7 @@ extern "C" int lg_spread_tile_resource_topk_f64(
     const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
     int64_t *io_idx, lg_stream_t stream) {
   LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls &&
-                 io_val && io_idx && n_users >= 0 && item_begin >= 0,
+                 io_val && io_idx && n_users >= 0 && n_users < 0x7fffffff && item_begin >= 0,
              "lg_spread_tile_resource_topk_f64: bad arguments");
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile &&
                  (int64_t)item_begin + width < 0x7fffffff,

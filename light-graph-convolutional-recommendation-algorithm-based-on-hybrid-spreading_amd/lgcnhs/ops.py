@@ -798,6 +798,9 @@ class TileWalk:
                  ex: RowSets | None, eu=None, ei=None, tile: int = 2048,
                  col_bounds: bool = True):
         self.A, self.u0, self.u1, self.i0, self.k, self.ex = A, u0, u1, i0, int(k), ex
+        # the walk keeps its stream positions in 32 bits
+        if A.by_user.col.numel() >= 2**31 or (ex is not None and ex.col.numel() >= 2**31):
+            raise ValueError("the tile walk needs fewer than 2^31 interactions / exclusions")
         self.n = u1 - u0
         self.dev = A.k_item.device
         self.vals = torch.full((self.n, self.k), float("-inf"), dtype=torch.float64,
