@@ -10,10 +10,11 @@
 //                      <= 0.00785 ||u|| ||j||           (gamma_128 = 128 * 2^-24)
 // so gb = max_{j in c} G_bf16 + 0.008 ||u|| max_{j in c} ||j|| (norms rounded up to fp32),
 // nudged up by 2^-22 relative for the fp32 operations that formed it, is an upper bound.
-// Per column (optional qb): q_j = ceil(255 (G_bf16_j + the same margin) / gb (1 + 2^-20)),
-// clamped to [0, 255], so gb * q_j / 255 >= G_chain_j as well (q_j = 0 when the bound is
-// <= 0; gb <= 0 makes every column's bound <= 0). Stored row-major, one byte per column,
-// rows of qstride bytes. (Folding the walk's rb_j / rbmax_c into q as well made the walk no
+// Per column (optional qb): q_j = rne(v_j + 0.5) >= v_j, v_j = 255 (G_bf16_j + the same
+// margin) / gb (1 + 2^-20), saturated to [0, 255] by v_cvt_pk_u8_f32 (measured on the box:
+// round to nearest even, negative / NaN -> 0, above 255 -> 255, scripts/micro/cvt_pk_u8.hip),
+// so gb * q_j / 255 >= G_chain_j as well (q_j = 0 when the bound is negative; gb <= 0 makes
+// every column's bound <= 0). Stored row-major, one byte per column, rows of qstride bytes. (Folding the walk's rb_j / rbmax_c into q as well made the walk no
 // faster -- 2.68 vs 2.67 s over the 489 C5 tiles -- and the bounds 0.34 s slower: dropped.)
 // Then fl(G_chain * F) <= fl(gb * F) for every F >= 0 (rounding is monotone), so a column
 // with gb * F <= tau can not beat tau. Cost per tile: 2 * U * T * D flop on bf16 MFMA
@@ -33,6 +34,14 @@ constexpr float kBoundMargin = 0.008f;
 #ifndef LG_BOUND_DEPTH
 #define LG_BOUND_DEPTH 1  // item-fragment chunks in flight ahead (2 measured no faster at D = 64)
 #endif
+
+// max of three floats without the NaN-quieting canonicalisation fmaxf adds (the operands are
+// finite or -inf)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float m;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+  return m;
+}
 
 __device__ __forceinline__ float round_up_f32(double x) {
   float f = (float)x;
@@ -159,12 +168,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      float m = fmaxf(fmaxf(accs[0][g][0], accs[0][g][1]), fmaxf(accs[0][g][2], accs[0][g][3]));
-#pragma unroll
-      for (int t = 1; t < 4; ++t)
-        m = fmaxf(fmaxf(m, fmaxf(accs[t][g][0], accs[t][g][1])),
-                  fmaxf(accs[t][g][2], accs[t][g][3]));
-      gmax[g] = m;
+      float m = max3f(accs[0][g][0], accs[0][g][1], accs[0][g][2]);
+      m = max3f(m, accs[0][g][3], accs[1][g][0]);
+      m = max3f(m, accs[1][g][1], accs[1][g][2]);
+      m = max3f(m, accs[1][g][3], accs[2][g][0]);
+      m = max3f(m, accs[2][g][1], accs[2][g][2]);
+      m = max3f(m, accs[2][g][3], accs[3][g][0]);
+      m = max3f(m, accs[3][g][1], accs[3][g][2]);
+      gmax[g] = fmaxf(m, accs[3][g][3]);
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -177,11 +188,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       const int64_t uu = ubase + 16 * g + ul;
       if (kg == 0 && uu < n_users) gb[uu * nch + c] = b;
       if (qb) {
-        // per column: q = ceil(v), v = fl(acc sc + msc) >= 255 (acc + marg) / b (sc and msc
-        // carry (1 + 2^-20) factors over their own roundings and the fma's), clamped to
-        // [0, 255]; 4 consecutive items of one user per lane and tile -> one dword
+        // per column: q = rne(v') with v' = fl(acc sc + msc) >= 255 (acc + marg) / b + 0.5 (sc
+        // and msc carry (1 + 2^-20) factors over their own roundings and the fma's; msc holds
+        // the 0.5 plus 1e-4 for the fma's absolute rounding near 0), so q >= the ratio; the
+        // conversion saturates to [0, 255]; 4 consecutive items of one user per lane and
+        // tile -> one dword
         const float sc = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) * (1.f + 0x1p-20f) : 0.f;
-        const float msc = marg * sc * (1.f + 0x1p-20f);
+        const float msc = (marg * sc * (1.f + 0x1p-20f) + 0.5001f) * (1.f + 0x1p-20f);
         const f32x2 sc2 = {sc, sc}, ms2 = {msc, msc};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -190,9 +203,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
           float v[4] = {lo[0], lo[1], hi[0], hi[1]};
           uint32_t w = 0;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            w = __builtin_amdgcn_cvt_pk_u8_f32(
-                __builtin_ceilf(__builtin_amdgcn_fmed3f(v[r], 0.f, 255.f)), r, w);
+          for (int r = 0; r < 4; ++r) w = __builtin_amdgcn_cvt_pk_u8_f32(v[r], r, w);
           // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair
           qs[(16 * g + ul) * QS + (c & 1) * 16 + 4 * t + kg] = w;
         }
