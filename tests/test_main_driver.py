@@ -78,8 +78,11 @@ def test_plot_metric_writes_png(tmp_path):
 def test_main_steps_1_to_3(cache_cfg, name):
     import main
     U, I = _write_cache(cache_cfg.PREPROCESSING["save_path"])
+    from const import Config
     cache_cfg.MODEL["name"] = name
-    cache_cfg.MODEL["HyperParameter"] = dict(cache_cfg.MODEL["HyperParameter"])
+    # the named model's own hyper-parameters (the reference's config classes carry one model's)
+    cache_cfg.MODEL["HyperParameter"] = dict(
+        Config(cache_cfg.ENV, cache_cfg.DATA_SET, name).MODEL["HyperParameter"])
     hp = cache_cfg.MODEL["HyperParameter"]
     if "epochs" in hp:
         hp.update(epochs=3, epoch_per_eval=2)
