@@ -31,9 +31,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBoundMargin = 0.008f;
-#ifndef LG_BOUND_DEPTH
-#define LG_BOUND_DEPTH 1  // item-fragment chunks in flight ahead (2 measured no faster at D = 64)
-#endif
 
 // max of three floats without the NaN-quieting canonicalisation fmaxf adds (the operands are
 // finite or -inf)
@@ -70,11 +67,13 @@ __global__ __launch_bounds__(256) void k_bound_prep(const float *__restrict__ x,
   if (lane == 0) norm[r] = round_up_f32(sqrt(ss) * (1.0 + 1e-12));
 }
 
-// One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile. W = waves per
-// SIMD the registers are sized for: D <= 64 runs 3 (152 VGPRs) and loads each chunk's item
-// fragments at its start (the other waves cover the latency; 393 vs 437 ms at C5 against 2
-// waves with the next chunk prefetched into 32 more registers), D = 128 runs 2 with the
-// prefetch (3 would spill).
+// One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile; a block = 4
+// waves = 256 users. The chunk's item fragments (64 items x D bf16) are shared by the block's
+// waves through LDS: the 256 threads load chunk c + 1 into registers while chunk c is computed
+// from its LDS buffer, store it into the other buffer afterwards, and one barrier per chunk
+// hands it over -- a quarter of the L2 fragment reads, and their latency hidden by a whole
+// chunk of work. W = waves per SIMD the registers and LDS are sized for (D <= 64: 3, D = 128:
+// 2). Waves past the last user still load and synchronise (their stores are masked).
 template <int D, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void k_chunk_bound(const __bf16 *__restrict__ ub,
                                                      const float *__restrict__ unorm,
@@ -86,8 +85,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
                                                      uint8_t *__restrict__ qb, int32_t qstride) {
   constexpr int S = D / 32;  // k-steps
   const int lane = lane_id();
-  const int64_t ubase = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 64;
-  if (ubase >= n_users) return;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));  // (uniform)
+  const int64_t ubase = ((int64_t)blockIdx.x * 4 + wv) * 64;
   const int ul = lane & 15, kg = lane >> 4;
   bf16x8 bfr[4][S];
   float un[4];
@@ -101,42 +100,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     un[g] = unorm[uu];
   }
   // q bytes of two chunks (64 users x 128 columns) staged in LDS, then written as whole
-  // 128-byte row segments (8 lanes x 16 bytes per user)
-  constexpr int QS = 36;  // dwords per user row: 32 + 4 (no bank conflicts, 16-B aligned)
-  __shared__ uint32_t qs_all[4][64 * QS];
-  uint32_t *qs = qs_all[threadIdx.x / 64];
-  // item fragments of a chunk: [tile t][k-step s]; the next chunk's are loaded while this
-  // chunk's MFMAs and bounds run
-  auto load_items = [&](int cb, bf16x8 (&fr)[4][S], float &nm) __attribute__((always_inline)) {
+  // 128-byte row segments (8 lanes x 16 bytes per user); 16-byte groups of a row swizzled by
+  // the row (2-way bank conflicts at most on the dword writes)
+  constexpr int QS = 32;  // dwords per user row
+  __shared__ __attribute__((aligned(16))) uint32_t qs_all[4][64 * QS];
+  uint32_t *qs = qs_all[wv];
+  // the staged chunks: 64 item rows of D bf16 (2 D bytes), written by LDS-DMA
+  // (global_load_lds_dwordx4: each wave instruction fills 1 KB contiguously, no VGPRs); the
+  // 16-byte pieces of row r sit XOR-swizzled by sw(r) = (r / (128 / D)) & (D / 8 - 1), so the
+  // fragment reads of any 16 consecutive lanes (16 rows, one piece) hit distinct banks
+  constexpr int PR = D / 8;               // 16-byte pieces per item row
+  constexpr int RB = 2 * D;               // bytes per staged row
+  constexpr int NL = 64 * PR / 256;       // DMA instructions per thread per chunk (D = 32: 1)
+  static_assert(NL >= 1 && 64 * PR % 256 == 0, "chunk pieces must spread over the block");
+  __shared__ __attribute__((aligned(16))) char frs[2][64 * RB];
+  auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
+  auto dma = [&](int cb, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      int it = cb + 16 * t + ul;  // A row = item
+    for (int j = 0; j < NL; ++j) {
+      const int u0 = 256 * j + 64 * wv;  // the wave's first 16-byte unit of this instruction
+      const int p = u0 + lane, r = p / PR;
+      int it = cb + r;
       it = it < width ? it : width - 1;
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        fr[t][s] = *reinterpret_cast<const bf16x8 *>(ib + (int64_t)(item_begin + it) * D +
-                                                     32 * s + 8 * kg);
+      const __bf16 *src = ib + (int64_t)(item_begin + it) * D + 8 * ((p % PR) ^ sw(r));
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(frs[buf] + 16 * u0));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
     }
-    nm = cb + lane < width ? inorm[item_begin + cb + lane] : 0.f;
   };
-  bf16x8 fa[4][S], fb[4][S];
-  float na = 0.f, nb = 0.f;
-  constexpr bool kNoPre = W >= 3;  // each chunk's fragments loaded at its start
-  if (!kNoPre) load_items(0, fa, na);
-  // D <= 64: chunk c + 2's fragments in flight during chunk c (c + 1's already landed);
-  // D = 128 keeps one chunk ahead (the registers of a third set would spill)
-  constexpr bool kDeep = LG_BOUND_DEPTH > 1 && D <= 64;
-  bf16x8 fc[4][S];
-  float nc = 0.f;
-  if (kDeep && nch > 1) load_items(64, fb, nb);
+  // the wave's 64 rows of gb through one descriptor (32-bit offsets)
+  const int64_t nrow_w = n_users - ubase < 64 ? n_users - ubase : 64;
+  const __amdgpu_buffer_rsrc_t rgb = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(gb + (ubase < n_users ? ubase : 0) * nch), 0,
+      nrow_w > 0 ? (int)(nrow_w * nch * 4) : 0, 0x00020000);
+  dma(0, 0);
+  float na = lane < width ? inorm[item_begin + lane] : 0.f;
+  // the DMA is inline asm, invisible to hipcc's waits: this wave's copies have landed only
+  // after an explicit vmcnt(0), which must precede the barrier that publishes the buffer
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int cb = 64 * c;  // chunk start inside the tile
-    if constexpr (kNoPre) {
-      load_items(cb, fa, na);
-    } else if constexpr (kDeep) {
-      if (c + 2 < nch) load_items(cb + 128, fc, nc);
-    } else {
-      if (c + 1 < nch) load_items(cb + 64, fb, nb);
+    float nb = 0.f;
+    if (c + 1 < nch) {
+      dma(cb + 64, (c + 1) & 1);  // into the buffer every wave finished reading at the last barrier
+      nb = cb + 64 + lane < width ? inorm[item_begin + cb + 64 + lane] : 0.f;
     }
     // the chunk's largest item norm (wave-uniform)
     float inm = na;
@@ -146,12 +157,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      // item tile t's A fragments from the staged chunk (read per tile: 8 S VGPRs live)
+      bf16x8 fa[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        fa[s] = *reinterpret_cast<const bf16x8 *>(frs[c & 1] + (16 * t + ul) * RB +
+                                                  16 * ((4 * s + kg) ^ sw(16 * t + ul)));
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][s], bfr[g][s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s], bfr[g][s], acc, 0, 0, 0);
         accs[t][g] = acc;
       }
     }
@@ -185,8 +202,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       const float marg = kBoundMargin * un[g] * inm;
       float b = m + marg;
       b += fabsf(b) * 0x1p-22f + 1e-30f;
-      const int64_t uu = ubase + 16 * g + ul;
-      if (kg == 0 && uu < n_users) gb[uu * nch + c] = b;
+      if (kg == 0)  // (rows past n_users: out of the descriptor's range, dropped)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, b), rgb,
+                                              (uint32_t)(4 * ((16 * g + ul) * nch + c)), 0, 0);
       if (qb) {
         // per column: q = rne(v') with v' = fl(acc sc + msc) >= 255 (acc + marg) / b + 0.5 (sc
         // and msc carry (1 + 2^-20) factors over their own roundings and the fma's; msc holds
@@ -204,39 +222,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
           uint32_t w = 0;
 #pragma unroll
           for (int r = 0; r < 4; ++r) w = __builtin_amdgcn_cvt_pk_u8_f32(v[r], r, w);
-          // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair
-          qs[(16 * g + ul) * QS + (c & 1) * 16 + 4 * t + kg] = w;
+          // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair (16-byte group
+          // 4 (c & 1) + t, swizzled by the row)
+          const int row = 16 * g + ul;
+          qs[row * QS + 4 * ((4 * (c & 1) + t) ^ (row & 7)) + kg] = w;
         }
       }
     }
     if (qb && ((c & 1) || c + 1 == nch)) {  // a chunk pair is complete: write it out
       wave_sync();
-      const int cp = 64 * (c & ~1);  // the pair's first column
+      const int cp = 64 * (c & ~1);  // the pair's first column (its 128 columns fit qstride)
+      // the wave's 64 q rows through one descriptor (rows past n_users are out of range:
+      // their stores are dropped), 32-bit offsets
+      const int64_t nrow = n_users - ubase < 64 ? n_users - ubase : 64;
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(qb + (ubase < n_users ? ubase : 0) * qstride), 0,
+          nrow > 0 ? (int)(nrow * qstride) : 0, 0x00020000);
 #pragma unroll
       for (int r8 = 0; r8 < 8; ++r8) {
         const int uloc = 8 * r8 + (lane >> 3);
-        const int64_t uu = ubase + uloc;
-        const int col = cp + 16 * (lane & 7);
-        const uint4 v = *reinterpret_cast<const uint4 *>(qs + uloc * QS + 4 * (lane & 7));
-        if (uu < n_users && col + 16 <= qstride)
-          *reinterpret_cast<uint4 *>(qb + uu * qstride + col) = v;
+        const uint4 v =
+            *reinterpret_cast<const uint4 *>(qs + uloc * QS + 4 * ((lane & 7) ^ (uloc & 7)));
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rq,
+            (uint32_t)(uloc * qstride + cp + 16 * (lane & 7)), 0, 0);
       }
       wave_sync();
     }
-    if constexpr (!kNoPre) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int s = 0; s < S; ++s) fa[t][s] = fb[t][s];
-      na = nb;
-    }
-    if constexpr (kDeep) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int s = 0; s < S; ++s) fb[t][s] = fc[t][s];
-      nb = nc;
-    }
+    na = nb;
+    // chunk c + 1's DMA (this wave's share) landed, then the barrier publishes the buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 }
 

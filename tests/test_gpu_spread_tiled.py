@@ -414,6 +414,36 @@ def test_find_lambda_api_rows(tmp_path):
 
 
 @pytest.mark.parametrize("d", [32, 64, 128])
+def test_score_bounds_cover_chain_scores_many_blocks(d):
+    """lg_score_chunk_bound at a launch of many blocks (65,536 users, a full 2048-column
+    tile of 32 chunks: the block's waves hand every chunk's item fragments over through
+    LDS): gb and gb * q / 255 cover the exact chain score of 384 sampled users (the first
+    and last blocks and random ones) on every column."""
+    from lgcnhs import ops
+    from oracle import lgcn_oracle as O
+    g = torch.Generator().manual_seed(100 + d)
+    U, W, j0 = 65536, 2048, 1000
+    eu = torch.randn(U, d, generator=g) * 0.1
+    ei = torch.randn(j0 + W + 7, d, generator=g) * 0.1
+    ub, un = ops.bound_operands(eu.to(DEV))
+    ib, inn = ops.bound_operands(ei.to(DEV))
+    q = torch.zeros((U, W), dtype=torch.uint8, device=DEV)
+    gb, q = ops.chunk_bounds(ub, un, ib, inn, d, j0, W, qout=q)
+    rs = np.random.default_rng(d)
+    users = np.unique(np.concatenate([np.arange(128), np.arange(U - 128, U),
+                                      rs.choice(U, 128, replace=False)]))
+    G = O.chain_scores(eu[users].numpy(), ei[j0:j0 + W].numpy()).astype(np.float64)
+    gbn = gb.cpu().numpy()[users].astype(np.float64)
+    qn = q.cpu().numpy()[users].astype(np.float64)
+    chunk = np.arange(W) // 64
+    assert np.all(gbn[:, chunk] >= G)
+    colb = gbn[:, chunk] * qn / 255.0
+    bad = colb < G
+    assert not bad.any(), (np.argwhere(bad)[:5], colb[bad][:5], G[bad][:5])
+    assert np.mean(colb - G) < np.mean(gbn[:, chunk] - G)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
 def test_score_bounds_cover_chain_scores(d):
     """lg_score_chunk_bound: the chunk bound gb and the per-column 8-bit bounds
     gb * q / 255 are >= the exact fp32 chain score (the C chain of oracle/score_chain.c) of
