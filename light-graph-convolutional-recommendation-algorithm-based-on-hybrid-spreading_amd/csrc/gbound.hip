@@ -33,11 +33,21 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float kBoundMargin = 0.008f;
 
 // max of three floats without the NaN-quieting canonicalisation fmaxf adds (the operands are
-// finite or -inf)
+// finite or -inf). Inline asm: hipcc pads no MFMA-result wait states before it, so the
+// caller retires the chunk's MFMAs first (mfma_settle)
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float m;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
   return m;
+}
+
+// every MFMA issued above has written its result before any instruction below reads it: no
+// instruction crosses the barriers, and 16 wait states >= the 12 an 8-pass XDL result needs
+// before a VALU read (cdna_hip_programming.md §5.7 item 2)
+__device__ __forceinline__ void mfma_settle() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ float round_up_f32(double x) {
@@ -172,6 +182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
         accs[t][g] = acc;
       }
     }
+    mfma_settle();
     // lane holds rows (items) 4 kg + r of each 16-item tile, column (user) ul; columns past
     // the width (a partial last chunk only) do not count
     if (cb + 64 > width) {

@@ -66,7 +66,13 @@ __device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items,
 }
 
 // max of the four scores of an MFMA result (plain v_max3/v_max: the NaN-quieting
-// canonicalisation fmaxf would add is irrelevant for a threshold test)
+// canonicalisation fmaxf would add is irrelevant for a threshold test). Inline asm: hipcc
+// pads no MFMA-result wait states before it, so it reads only results an MFMA wrote well
+// before (k_score_topk's filter runs one tile behind its MFMAs); right after an MFMA,
+// max4_fresh (compiler-visible: hipcc inserts the wait states).
+__device__ __forceinline__ float max4_fresh(f32x4 a) {
+  return fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+}
 __device__ __forceinline__ float max4(f32x4 a) {
   float m;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a[0]), "v"(a[1]), "v"(a[2]));
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (__ballot(max4(acc[g]) > thr[g]) == 0) continue;
+      if (__ballot(max4_fresh(acc[g]) > thr[g]) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float sc = acc[g][r];
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     }
     bool hit = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) hit |= max4(accb[g]) + marg[g] > thr[g];
+    for (int g = 0; g < NG; ++g) hit |= max4_fresh(accb[g]) + marg[g] > thr[g];
     if (__ballot(hit)) {
       exact_tile(t);
       const int l = (int)i0 + (t + 1) * 16;
