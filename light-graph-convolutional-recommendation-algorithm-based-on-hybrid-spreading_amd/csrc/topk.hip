@@ -397,6 +397,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
+  // compact (and raise the threshold) once k + 12 candidates are held: the screen's hit
+  // rate follows the threshold
+  const int trig = k + 12 < CAP - 16 ? k + 12 : CAP - 16;
 
   // (k_score_topk's lazy exclusion and compaction, unchanged)
   auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
@@ -443,11 +446,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
     bool over = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > trig;
     if (__ballot(over) == 0) return;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+      uint64_t need = __ballot(cnt[g] > trig) & 0xffffull;
       if (need) {
         wave_sync();
         while (need) {
@@ -467,26 +470,44 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       fr[s] = *reinterpret_cast<const bf16x8 *>(eib + it * D + 32 * s + 8 * gq);
   };
   // the exact tile: k_score_topk's f32 chain, then its insertion against thr
-  auto exact_tile = [&](int t) __attribute__((always_inline)) {
+  // (only the user groups whose screen hit: a group's chain is its own 16-user MFMA column
+  // block, so the others' exact scores are not needed)
+  auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
     int64_t it = i0 + 16 * t + ul;
     it = it < n_items ? it : n_items - 1;
     float af[Q];
     load_piece<Q>(ei + it * D + gq * Q, af);
-    f32x4 acc[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < Q; ++s)
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], acc[g], 0, 0, 0);
     const int rel = t * 16 + gq * 4;
+    bool all = true;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) all &= gh[g];
+    f32x4 accs[NG];
+    if (all) {  // every group: the chains interleave on the MFMA pipe
+#pragma unroll
+      for (int g = 0; g < NG; ++g) accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < Q; ++s)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!gh[g]) continue;  // (wave-uniform)
+#pragma unroll
+        for (int s = 0; s < Q; ++s)
+          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (__ballot(max4_fresh(acc[g]) > thr[g]) == 0) continue;
+      if (!gh[g]) continue;
+      const f32x4 acc = accs[g];
+      if (__ballot(max4_fresh(acc) > thr[g]) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float sc = acc[g][r];
+        const float sc = acc[r];
         const bool cand = rel + r < n_valid && sc > thr[g];
         const uint64_t bal = __ballot(cand);
         if (bal) {
@@ -520,11 +541,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       if (t & 1) load_bf(t + 2, fb);
       else load_bf(t + 2, fa);
     }
+    bool gh[NG];
     bool hit = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) hit |= max4_fresh(accb[g]) + marg[g] > thr[g];
-    if (__ballot(hit)) {
-      exact_tile(t);
+    for (int g = 0; g < NG; ++g) {
+      gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+      hit |= gh[g];
+    }
+    if (hit) {
+      exact_tile(t, gh);
       const int l = (int)i0 + (t + 1) * 16;
       maybe_compact(l < lim_end ? l : lim_end);
     }
