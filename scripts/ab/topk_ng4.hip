@@ -523,40 +523,35 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   };
 
   const int lim_end = (int)i1;
-  // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
-  // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
-  // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at C5,
-  // d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
-  bf16x8 fr[2][S];
-  load_bf(0, fr[0]);
-  load_bf(1, fr[1]);
-  for (int t0 = 0; t0 < n_t; t0 += 2) {
+  bf16x8 fa[S], fb[S];
+  if (n_t > 0) load_bf(0, fa);
+  if (n_t > 1) load_bf(1, fb);
+  for (int t = 0; t < n_t; ++t) {
+    f32x4 accb[NG];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int t = t0 + p;
-      if (t >= n_t) break;
-      f32x4 accb[NG];
+    for (int g = 0; g < NG; ++g) {
+      accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s)
+        accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((t & 1) ? fb[s] : fa[s], ub[g][s],
+                                                          accb[g], 0, 0, 0);
+    }
+    // tile t + 2 into the buffer tile t just left
+    if (t + 2 < n_t) {
+      if (t & 1) load_bf(t + 2, fb);
+      else load_bf(t + 2, fa);
+    }
+    bool gh[NG];
+    bool hit = false;
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[p][s], ub[g][s], accb[g], 0, 0, 0);
-      }
-      // tile t + 2 into the buffer tile t just left
-      load_bf(t + 2, fr[p]);
-      bool gh[NG];
-      bool hit = false;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
-        hit |= gh[g];
-      }
-      if (hit) {
-        exact_tile(t, gh);
-        const int l = (int)i0 + (t + 1) * 16;
-        maybe_compact(l < lim_end ? l : lim_end);
-      }
+    for (int g = 0; g < NG; ++g) {
+      gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+      hit |= gh[g];
+    }
+    if (hit) {
+      exact_tile(t, gh);
+      const int l = (int)i0 + (t + 1) * 16;
+      maybe_compact(l < lim_end ? l : lim_end);
     }
   }
 
@@ -763,7 +758,7 @@ static void dispatch_topk_screen(int M, const float *eu, const float *ei, const 
                                                   items_per_split, out_val, out_idx, part_val, \
                                                   part_idx);                                  \
   }
-  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 4)
+  if (M == 1) LG_SCREEN_LAUNCH(4, 1, 2)
   else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2)
   else LG_SCREEN_LAUNCH(1, 4, 2)
 #undef LG_SCREEN_LAUNCH

@@ -339,6 +339,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
 // user's list can still take the mask value (thr = -inf) every tile is recomputed.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef RING
+#define RING 2
+#endif
 template <int D, int NG, int M, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
@@ -523,16 +526,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   };
 
   const int lim_end = (int)i1;
-  // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
-  // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
-  // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at C5,
-  // d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
-  bf16x8 fr[2][S];
-  load_bf(0, fr[0]);
-  load_bf(1, fr[1]);
-  for (int t0 = 0; t0 < n_t; t0 += 2) {
+  // a ring of R tiles' bf16 fragments in flight (every load issued, clamped past the end,
+  // so the wait before tile t counts the younger tiles' loads instead of draining them)
+  constexpr int R = D <= 64 ? RING : 2;
+  bf16x8 fr[R][S];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
+  for (int p = 0; p < R; ++p) load_bf(p, fr[p]);
+  for (int t0 = 0; t0 < n_t; t0 += R) {
+#pragma unroll
+    for (int p = 0; p < R; ++p) {
       const int t = t0 + p;
       if (t >= n_t) break;
       f32x4 accb[NG];
@@ -543,8 +545,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
         for (int s = 0; s < S; ++s)
           accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[p][s], ub[g][s], accb[g], 0, 0, 0);
       }
-      // tile t + 2 into the buffer tile t just left
-      load_bf(t + 2, fr[p]);
+      // tile t + R into the buffer tile t just left
+      load_bf(t + R, fr[p]);
       bool gh[NG];
       bool hit = false;
 #pragma unroll

@@ -24,7 +24,18 @@ ap.add_argument("--no-col-bounds", action="store_true",
                 help="chunk score bounds only (no per-column 8-bit bounds)")
 ap.add_argument("--no-excl", action="store_true",
                 help="no exclusion sets (timing of the walk without the per-user exclusion cursor)")
+ap.add_argument("--identity-classes", action="store_true",
+                help="class = degree (the walk_recip A/B variant computes fl(1/k) itself)")
 a = ap.parse_args()
+if a.identity_classes:
+    def _identity_classes(deg):
+        n = max(ops.INV_TAB, int(deg.max()) + 1)
+        if n > ops.MAX_CLASSES:
+            raise ValueError("degree too large for identity classes")
+        inv = torch.zeros(n, dtype=torch.float64, device=deg.device)
+        inv[1:] = 1.0 / torch.arange(1, n, dtype=torch.float64, device=deg.device)
+        return deg.to(torch.int16).view(torch.uint16), inv
+    ops.degree_classes = _identity_classes
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
 _, _, keys = bench.gen_graph(U, I, E, 0, dev)
