@@ -339,7 +339,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
 // user's list can still take the mask value (thr = -inf) every tile is recomputed.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int D, int NG, int M, int WAVES>
+template <int D, int NG, int M, int WAVES, bool SH>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
     const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
@@ -361,7 +361,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   const int64_t tile = blockIdx.x / n_splits;
   const int split = blockIdx.x % n_splits;
   const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
-  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  // (SH: waves past the last user still stage their share of every chunk and meet every
+  // barrier; their users are invalid, so they never hit the screen and write nothing)
+  if (!SH && ubase >= n_users) return;  // wave-uniform; no block-level barriers below
   const int64_t i0 = (int64_t)split * items_per_split;
   int64_t i1 = i0 + items_per_split;
   if (i1 > n_items) i1 = n_items;
@@ -523,39 +525,93 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   };
 
   const int lim_end = (int)i1;
-  // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
-  // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
-  // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at C5,
-  // d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
-  bf16x8 fr[2][S];
-  load_bf(0, fr[0]);
-  load_bf(1, fr[1]);
-  for (int t0 = 0; t0 < n_t; t0 += 2) {
+  // tile t: the bf16 screen of its fragments fr, then (rarely) the exact tile and compaction
+  auto screen_tile = [&](int t, const bf16x8 (&fr)[S], auto &&after_mfma)
+      __attribute__((always_inline)) {
+    f32x4 accb[NG];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int t = t0 + p;
-      if (t >= n_t) break;
-      f32x4 accb[NG];
+    for (int g = 0; g < NG; ++g) {
+      accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s)
+        accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s], ub[g][s], accb[g], 0, 0, 0);
+    }
+    after_mfma();
+    bool gh[NG];
+    bool hit = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+      hit |= gh[g];
+    }
+    if (hit) {
+      exact_tile(t, gh);
+      const int l = (int)i0 + (t + 1) * 16;
+      maybe_compact(l < lim_end ? l : lim_end);
+    }
+  };
+  if constexpr (SH) {
+    // The block's waves share the bf16 item fragments through LDS: chunks of CI items
+    // (8 KiB, one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a
+    // ring of 3 buffers, chunk c + 2 issued while chunk c is screened; the 16-byte pieces of
+    // row r stored XOR-swizzled by sw(r) through the SOURCE address, so the fragment reads of
+    // any 16 consecutive lanes hit distinct banks (the layout of csrc/gbound.hip). The DMA is
+    // inline asm, invisible to hipcc's waits: each wave waits for its own piece of chunk
+    // c + 1 (vmcnt(1): all but the youngest vector-memory op -- chunk c + 2's piece, or
+    // nothing if the exact path loaded after it) before the barrier that publishes it.
+    constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D, NBUF = 3;
+    static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
+    __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
+    auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
+    const int pp = (int)threadIdx.x, pr = pp / PR;
+    const int pcol = 8 * ((pp % PR) ^ sw(pr));
+    auto dma = [&](int c, int buf) __attribute__((always_inline)) {
+      int64_t it = i0 + (int64_t)c * CI + pr;
+      it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
+      const __bf16 *src = eib + it * D + pcol;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(frs[buf] + 1024 * wave));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    };
+    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform: every wave meets every barrier)
+    dma(0, 0);
+    dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c < n_c; ++c) {
+      dma(c + 2, (c + 2) % NBUF);  // into chunk c - 1's buffer (released by the last barrier)
+      const char *fb = frs[c % NBUF];
+      for (int tt = 0; tt < TPC; ++tt) {
+        const int t = c * TPC + tt;
+        if (t >= n_t) break;
+        bf16x8 fr[S];
+        const int r = 16 * tt + ul;
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[p][s], ub[g][s], accb[g], 0, 0, 0);
+          fr[s] = *reinterpret_cast<const bf16x8 *>(fb + r * RB + 16 * ((4 * s + gq) ^ sw(r)));
+        screen_tile(t, fr, [] {});
       }
-      // tile t + 2 into the buffer tile t just left
-      load_bf(t + 2, fr[p]);
-      bool gh[NG];
-      bool hit = false;
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
+    // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
+    // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at
+    // C5, d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
+    bf16x8 fr[2][S];
+    load_bf(0, fr[0]);
+    load_bf(1, fr[1]);
+    for (int t0 = 0; t0 < n_t; t0 += 2) {
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
-        hit |= gh[g];
-      }
-      if (hit) {
-        exact_tile(t, gh);
-        const int l = (int)i0 + (t + 1) * 16;
-        maybe_compact(l < lim_end ? l : lim_end);
+      for (int p = 0; p < 2; ++p) {
+        const int t = t0 + p;
+        if (t >= n_t) break;
+        // tile t + 2 into the buffer tile t just left, right after tile t's MFMAs
+        screen_tile(t, fr[p], [&] { load_bf(t + 2, fr[p]); });
       }
     }
   }
@@ -753,19 +809,21 @@ static void dispatch_topk_screen(int M, const float *eu, const float *ei, const 
                                  const int32_t *ex_col, float mask_value, int k, int n_splits,
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
                                  float *part_val, int32_t *part_idx, hipStream_t stream) {
-#define LG_SCREEN_LAUNCH(NG, MM, W)                                                            \
+#define LG_SCREEN_LAUNCH(NG, MM, W, SH)                                                        \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_score_topk_screen<D, NG, MM, W><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, \
+    k_score_topk_screen<D, NG, MM, W, SH><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, \
                                         stream>>>(eu, ei, eub, eib, umarg, n_users, n_items,  \
                                                   ex_rowptr, ex_col, mask_value, k, n_splits, \
                                                   items_per_split, out_val, out_idx, part_val, \
                                                   part_idx);                                  \
   }
-  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 4)
-  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2)
-  else LG_SCREEN_LAUNCH(1, 4, 2)
+  // k <= 32: one 8-wave block per CU (128 KiB of lists + the 24 KiB fragment ring) shares
+  // the item fragments; larger lists keep 2-wave blocks that load their own
+  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 8, true)
+  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2, false)
+  else LG_SCREEN_LAUNCH(1, 4, 2, false)
 #undef LG_SCREEN_LAUNCH
 }
 

@@ -168,19 +168,30 @@ def propagate(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------ scoring
-def _resident_blocks(device) -> int:
-    """Workgroups of lg_score_topk_f32 resident at once: 64 KiB of LDS each -> 2 per CU."""
-    return 2 * torch.cuda.get_device_properties(device).multi_processor_count
+def _resident_blocks(device, k: int = 64, screen: bool = False) -> int:
+    """Workgroups resident at once: lg_score_topk_f32's (and the screened kernel's for
+    k > 32) take 64 KiB of LDS -> 2 per CU; the screened kernel's 8-wave blocks for k <= 32
+    take 154 KiB -> 1 per CU."""
+    per_cu = 1 if (screen and k <= 32) else 2
+    return per_cu * torch.cuda.get_device_properties(device).multi_processor_count
 
 
-def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512) -> int:
+def _users_per_block(k: int, screen: bool = False) -> int:
+    """Users per workgroup of csrc/topk.hip's launches (dispatch_topk / _screen)."""
+    if screen and k <= 32:
+        return 256
+    return 128 if k <= 32 else (64 if k <= 64 else 32)
+
+
+def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512,
+                screen: bool = False) -> int:
     """Item-range splits for lg_score_topk_f32: the fewest splits that keep every CU busy.
 
     Each split restarts every user's candidate list from an empty threshold (the warm-up
     inserts ~k*ln(items/k) candidates), so more splits cost work; too few leave CUs idle
     in the last round of workgroups. Minimise rounds/splits (the makespan in units of one
     unsplit block) with a 2 % penalty per split."""
-    per_block = 128 if k <= 32 else (64 if k <= 64 else 32)
+    per_block = _users_per_block(k, screen)
     tiles = (n_users + per_block - 1) // per_block
     best, best_cost = 1, None
     for s in range(1, min(64, max(1, n_items // 256)) + 1):
@@ -214,8 +225,8 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
         raise ValueError("eu/ei dims differ")
     if excl is not None and excl.n_rows != nu:
         raise ValueError(f"exclusion rows {excl.n_rows} != users {nu}")
-    ns = (_splits_for(nu, ni, k, _resident_blocks(eu.device)) if n_splits is None
-          else int(n_splits))
+    ns = (_splits_for(nu, ni, k, _resident_blocks(eu.device, k, screen), screen)
+          if n_splits is None else int(n_splits))
     ws_bytes = N.lib().lg_score_topk_ws_bytes(nu, ni, d, k, ns)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
     val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)

@@ -26,7 +26,7 @@ for D in (64, 128):
     ub, un = ops.bound_operands(eu)
     ib, inorm = ops.bound_operands(ei)
     real = un * (inorm.max() * ops.SCREEN_MARGIN)
-    ns = ops._splits_for(U, I, k, ops._resident_blocks(dev))
+    ns = ops._splits_for(U, I, k, ops._resident_blocks(dev, k, True), True)
     wsb = N.lib().lg_score_topk_ws_bytes(U, I, D, k, ns)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     val = torch.empty((U, k), dtype=torch.float32, device=dev)
