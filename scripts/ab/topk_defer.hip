@@ -1,0 +1,1057 @@
+// K2: full-catalog scoring + exclusion mask + streaming top-K, gfx950 f32 MFMA.
+//
+// Replaces model/LightGCN/recommend.py:83-114 (identical in LightGCNOpti/recommend.py and
+// LightGCN/evaluation.py:31-51):
+//     score = torch.matmul(users_emb.weight, items_emb.weight.T)       # [U, I] fp32
+//     score[train positives] = -(1 << 10); score[val positives] = -(1 << 10)
+//     _, recommendations = torch.topk(score, k)
+// and the dense masked matrix of getAllocateMat (model/SpreadLightGCN/model.py:74-104).
+//
+// Score definition (bit-exact, checked against oracle/score_chain.c): v_mfma_f32_16x16x4_f32
+// computes a k-ordered fp32 fma chain. Lane l of a wave holds item row (l & 15) as the A
+// operand and user column (l & 15) as the B operand, k-slot (l >> 4); step s of the chain
+// uses element g*Q + s of k-slot g (Q = D/4), so each lane reads one contiguous 16*Q-byte
+// piece of each embedding row, and the fp32 result equals
+//     acc = 0; for s < Q: for g < 4: acc = fmaf(u[g*Q+s], i[g*Q+s], acc).
+// Top-K: per user a candidate list of CAP entries in LDS; a score enters only if it beats
+// the user's current K-th best (tau), so after the first few hundred items almost nothing
+// enters and the VALU cost per score is one compare. The exclusion row (sorted) is
+// binary-searched only for list entries, in batch when the list is compacted: an excluded
+// item takes mask_value (-1024) before the sort, which is exactly the reference's masked
+// top-k. Lists are compacted by the wave-wide bitonic sort of common.h. Order: (score
+// desc, item asc). The main loop thus issues no global load but the item tiles.
+#include <stdlib.h>
+
+#include "common.h"
+
+namespace lg {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int Q>
+__device__ __forceinline__ void load_piece(const float *__restrict__ p, float (&v)[Q]) {
+  const float4 *p4 = reinterpret_cast<const float4 *>(p);
+#pragma unroll
+  for (int t = 0; t < Q / 4; ++t) {
+    const float4 q = p4[t];
+    v[4 * t + 0] = q.x;
+    v[4 * t + 1] = q.y;
+    v[4 * t + 2] = q.z;
+    v[4 * t + 3] = q.w;
+  }
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// Item-tile loads: buffer_load through a per-tile descriptor whose base is the tile's first
+// row and whose record count is the bytes left in the table (0 past its end), so rows
+// beyond n_items read as 0 and every tile issues the same LT loads with no branch and no
+// per-lane address arithmetic. Inline asm keeps them invisible to the compiler's wait
+// analysis (cdna_hip_programming.md §5.7 item 1); the caller waits by hand with
+// wait_vm<N>() = "all but the N youngest vector-memory ops".
+template <int D>
+__device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items, int64_t it,
+                                               int voff, f32x4v (&v)[D / 16]) {
+  constexpr int TB = 16 * D * 4;  // bytes of one 16-item tile
+  const int rem = (int)(n_items - it);  // items left in the table (n_items < 2^31)
+  const int num = rem >= 16 ? TB : (rem > 0 ? rem * (D * 4) : 0);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(ei + it * D), 0, num, 0x00020000);
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3"
+                 : "=v"(v[t])
+                 : "v"(voff), "s"(r), "i"(t * 16)
+                 : "memory");
+}
+
+// max of the four scores of an MFMA result (plain v_max3/v_max: the NaN-quieting
+// canonicalisation fmaxf would add is irrelevant for a threshold test). Inline asm: hipcc
+// pads no MFMA-result wait states before it, so it reads only results an MFMA wrote well
+// before (k_score_topk's filter runs one tile behind its MFMAs); right after an MFMA,
+// max4_fresh (compiler-visible: hipcc inserts the wait states).
+__device__ __forceinline__ float max4_fresh(f32x4 a) {
+  return fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+}
+__device__ __forceinline__ float max4(f32x4 a) {
+  float m;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a[0]), "v"(a[1]), "v"(a[2]));
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(m), "v"(a[3]));
+  return m;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (§5.4 rule 18)
+}
+
+// One wave: NG groups of 16 users; the block's waves work independently.
+//
+// Software pipeline (per wave, one 16-item tile per step t):
+//   wait for tile t+1  ->  MFMAs of tile t+1 into acc[(t+1)%2], interleaved with the
+//   one-max-one-compare filter of tile t's scores in acc[t%2]  ->  issue the loads of tile
+//   t+3 into the register buffer tile t+1 just left  ->  (rare) insert tile t's candidates
+//   ->  compact lists that could overflow.
+// The filter's vector instructions fill the MFMA issue gaps (an f32 16x16x4 MFMA holds the
+// SIMD's vector issue for 8 of its 32 cycles), and each tile's loads are in flight for two
+// steps.
+template <int D, int NG, int M, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_score_topk(
+    const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
+    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx, int probe) {
+  constexpr int Q = D / 4;
+  constexpr int LT = Q / 4;  // buffer loads per tile per lane
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[WAVES][NG][16][CAP];
+  __shared__ int ci[WAVES][NG][16][CAP];
+  __shared__ int exs[WAVES][64];
+
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  const int64_t tile = blockIdx.x / n_splits;
+  const int split = blockIdx.x % n_splits;
+  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
+  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  const int64_t i0 = (int64_t)split * items_per_split;
+  int64_t i1 = i0 + items_per_split;
+  if (i1 > n_items) i1 = n_items;
+  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;  // items of this split
+  const int n_t = (n_valid + 15) / 16;                // tiles of this split
+
+  float uf[NG][Q];
+  bool uvalid[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
+  int cnt[NG], chk[NG];
+  float tau[NG], thr[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t u = ubase + g * 16 + ul;
+    uvalid[g] = u < n_users;
+    const int64_t uu = uvalid[g] ? u : n_users - 1;
+    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+    ex_pos[g] = 0;
+    ex_hi[g] = 0;
+    if (ex_rowptr && uvalid[g]) {
+      ex_pos[g] = ex_rowptr[u];
+      ex_hi[g] = ex_rowptr[u + 1];
+    }
+    cnt[g] = 0;
+    chk[g] = 0;
+    tau[g] = neg_inf<float>();
+    thr[g] = (uvalid[g] && probe != 1) ? neg_inf<float>() : __builtin_huge_valf();
+    // probe == 1 (measurement builds only, see topk_probe()): no candidate ever enters
+  }
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+
+  // Exclusion is applied lazily: a candidate enters on its raw score (or on the mask value
+  // when that alone beats tau), and the entries [chk, n) added since the user's last
+  // compaction are checked when the list is compacted. Their items all lie in
+  // [previous limit, lim), and ex_pos is the user's first excluded item not yet passed
+  // (>= the previous limit, or the row start: items below i0 are harmless), so the
+  // excluded items to test are one ascending run ex_col[ex_pos ..) read 64 at a time,
+  // coalesced, and binary-searched in LDS. Exact: an excluded item would enter with
+  // mask_value, and mask_value > tau admits every item.
+  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
+    const int n = __shfl(cnt[g], u);
+    const int c0 = __shfl(chk[g], u);
+    int64_t pos = __shfl(ex_pos[g], u);
+    const int64_t hi = __shfl(ex_hi[g], u);
+    float *ks = &cs[wave][g][u][0];
+    int *is = &ci[wave][g][u][0];
+    if (n > c0) {
+      while (pos < hi) {
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        const int nin = __popcll(__ballot(x < lim));  // ascending: a prefix of the lanes
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        for (int j = c0 + lane; j < n; j += 64) {
+          const int item = is[j];
+          int a = 0, b = nin;  // first index with exs[] >= item
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) ks[j] = mask_value;
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
+      }
+    }
+    float t;
+    int tid;
+    const int nc = wave_compact<float, M>(ks, is, n, k, t, tid);
+    if (ul == u) {
+      cnt[g] = nc;
+      chk[g] = nc;
+      tau[g] = t;
+      ex_pos[g] = pos;
+      // a masked (excluded) item would enter with mask_value: admit everything then
+      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
+    }
+  };
+
+  // acc[g][r] = score(user ubase + 16g + ul, item i0 + 16t + 4gq + r)
+  auto mfma_tile = [&](const f32x4v(&af)[LT], f32x4 (&acc)[NG]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // s outer / g inner: NG independent accumulation chains interleave on the MFMA pipe
+#pragma unroll
+    for (int s = 0; s < Q; ++s)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s / 4][s % 4], uf[g][s], acc[g], 0,
+                                                      0, 0);
+  };
+
+  // Fast filter: one max and one compare per group against thr = the entry threshold (tau,
+  // or -inf while the mask value itself would enter, +inf for padding users).
+  auto any_cand = [&](const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) any |= max4(acc[g]) > thr[g];
+    return __ballot(any) != 0;
+  };
+
+  // Slow path, taken when some lane of the wave has a candidate in tile t.
+  auto insert_tile = [&](int t, const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
+    const int rel = t * 16 + gq * 4;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (__ballot(max4(acc[g]) > thr[g]) == 0) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = acc[g][r];
+        const bool cand = rel + r < n_valid && sc > thr[g];
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][pos] = sc;
+            ci[wave][g][ul][pos] = (int)i0 + rel + r;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+  };
+
+  // compact every user whose list could overflow on the next tile (+16 max per tile)
+  auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+    if (__ballot(over) == 0) return;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      uint64_t need = __ballot(cnt[g] > CAP - 16) & 0xffffull;
+      if (need) {
+        wave_sync();
+        while (need) {
+          const int u = __ffsll((long long)need) - 1;
+          need &= need - 1;
+          compact_user(g, u, lim);
+        }
+      }
+    }
+  };
+
+  const int voff = (ul * D + gq * Q) * 4;
+  const int lim_end = (int)i1;
+  auto step_lim = [&](int t) __attribute__((always_inline)) {
+    const int l = (int)i0 + (t + 1) * 16;
+    return l < lim_end ? l : lim_end;
+  };
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the prologue loads: vmcnt(0)
+  if (n_t > 0) {
+    f32x4v afA[LT], afB[LT];
+    f32x4 accA[NG], accB[NG];
+    load_item_tile<D>(ei, n_items, i0, voff, afA);
+    load_item_tile<D>(ei, n_items, i0 + 16, voff, afB);
+    wait_vm<LT>();
+    mfma_tile(afA, accA);
+    load_item_tile<D>(ei, n_items, i0 + 32, voff, afA);
+    // invariant at step t: acc[t%2] = tile t; buffer (t+1)%2 = tile t+1 (landed or in
+    // flight); buffer t%2 = tile t+2 in flight
+    for (int t = 0;; t += 2) {
+      // ---- even step: tile t in accA, tile t+1 in afB
+      wait_vm<LT>();
+      mfma_tile(afB, accB);
+      bool hit = any_cand(accA);
+      load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 3) * 16, voff, afB);
+      if (hit) insert_tile(t, accA);
+      maybe_compact(step_lim(t));
+      if (t + 1 >= n_t) break;
+      // ---- odd step: tile t+1 in accB, tile t+2 in afA
+      wait_vm<LT>();
+      mfma_tile(afA, accA);
+      hit = any_cand(accB);
+      load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 4) * 16, voff, afA);
+      if (hit) insert_tile(t + 1, accB);
+      maybe_compact(step_lim(t + 1));
+      if (t + 2 >= n_t) break;
+    }
+  }
+  wait_vm<0>();
+
+  // final lists
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t user = ubase + g * 16 + u;
+      if (user >= n_users) break;
+      compact_user(g, u, lim_end);
+      const int nc = __shfl(cnt[g], u);
+      for (int e = lane; e < k; e += 64) {
+        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
+        const int id = e < nc ? ci[wave][g][u][e] : -1;
+        if (n_splits == 1) {
+          out_val[user * k + e] = v;
+          out_idx[user * k + e] = id;
+        } else {
+          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          part_val[o] = v;
+          part_idx[o] = id;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+// K2s: the same top-K with a bf16 MFMA screen (v_mfma_f32_16x16x32_bf16, 16x the f32
+// MFMA's rate). Per 16-item tile every user's bf16 product plus a rigorous margin m_u
+// (|G_bf16 - G_chain| <= 0.00785 ||u|| ||i||, csrc/gbound.hip; m_u = 0.0081 ||u|| max ||i||
+// >= it) is an upper bound of the exact fp32 chain score. Only a tile where some user's bound
+// beats its entry threshold is recomputed with the f32 MFMA chain of k_score_topk -- the
+// exact scores, bit for bit -- and runs k_score_topk's insertion on them. A tile that is not
+// recomputed holds no score above any threshold, so k_score_topk would have inserted
+// nothing from it either: the lists (values, ids, order) are k_score_topk's exactly. While a
+// user's list can still take the mask value (thr = -inf) every tile is recomputed.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int D, int NG, int M, int WAVES, bool SH>
+__global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
+    const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
+    const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
+    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
+  constexpr int Q = D / 4;   // f32 MFMA steps
+  constexpr int S = D / 32;  // bf16 MFMA k-blocks
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[WAVES][NG][16][CAP];
+  __shared__ int ci[WAVES][NG][16][CAP];
+  __shared__ int exs[WAVES][64];
+
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  const int64_t tile = blockIdx.x / n_splits;
+  const int split = blockIdx.x % n_splits;
+  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
+  // (SH: waves past the last user still stage their share of every chunk and meet every
+  // barrier; their users are invalid, so they never hit the screen and write nothing)
+  if (!SH && ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  const int64_t i0 = (int64_t)split * items_per_split;
+  int64_t i1 = i0 + items_per_split;
+  if (i1 > n_items) i1 = n_items;
+  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;
+  const int n_t = (n_valid + 15) / 16;
+
+  float uf[NG][Q];
+  bf16x8 ub[NG][S];
+  float marg[NG];
+  bool uvalid[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
+  int cnt[NG], chk[NG];
+  float tau[NG], thr[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t u = ubase + g * 16 + ul;
+    uvalid[g] = u < n_users;
+    const int64_t uu = uvalid[g] ? u : n_users - 1;
+    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
+    marg[g] = umarg[uu];
+    ex_pos[g] = 0;
+    ex_hi[g] = 0;
+    if (ex_rowptr && uvalid[g]) {
+      ex_pos[g] = ex_rowptr[u];
+      ex_hi[g] = ex_rowptr[u + 1];
+    }
+    cnt[g] = 0;
+    chk[g] = 0;
+    tau[g] = neg_inf<float>();
+    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
+  }
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+  // compact (and raise the threshold) once k + 12 candidates are held: the screen's hit
+  // rate follows the threshold
+  const int trig = k + 12 < CAP - 16 ? k + 12 : CAP - 16;
+
+  // (k_score_topk's lazy exclusion and compaction, unchanged)
+  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
+    const int n = __shfl(cnt[g], u);
+    const int c0 = __shfl(chk[g], u);
+    int64_t pos = __shfl(ex_pos[g], u);
+    const int64_t hi = __shfl(ex_hi[g], u);
+    float *ks = &cs[wave][g][u][0];
+    int *is = &ci[wave][g][u][0];
+    if (n > c0) {
+      while (pos < hi) {
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        const int nin = __popcll(__ballot(x < lim));
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        for (int j = c0 + lane; j < n; j += 64) {
+          const int item = is[j];
+          int a = 0, b = nin;
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) ks[j] = mask_value;
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
+      }
+    }
+    float t;
+    int tid;
+    const int nc = wave_compact<float, M>(ks, is, n, k, t, tid);
+    if (ul == u) {
+      cnt[g] = nc;
+      chk[g] = nc;
+      tau[g] = t;
+      ex_pos[g] = pos;
+      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
+    }
+  };
+  auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) over |= cnt[g] > trig;
+    if (__ballot(over) == 0) return;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      uint64_t need = __ballot(cnt[g] > trig) & 0xffffull;
+      if (need) {
+        wave_sync();
+        while (need) {
+          const int u = __ffsll((long long)need) - 1;
+          need &= need - 1;
+          compact_user(g, u, lim);
+        }
+      }
+    }
+  };
+  // bf16 fragments of tile t: lane (ul, gq) holds item ul's elements 32 s + 8 gq .. + 7
+  auto load_bf = [&](int t, bf16x8 (&fr)[S]) __attribute__((always_inline)) {
+    int64_t it = i0 + 16 * t + ul;
+    it = it < n_items ? it : n_items - 1;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      fr[s] = *reinterpret_cast<const bf16x8 *>(eib + it * D + 32 * s + 8 * gq);
+  };
+  // the exact tile: k_score_topk's f32 chain, then its insertion against thr
+  // (only the user groups whose screen hit: a group's chain is its own 16-user MFMA column
+  // block, so the others' exact scores are not needed)
+  // fp32 fragments of tile t (clamped past the table)
+  auto load_exact = [&](int t, float (&af)[Q]) __attribute__((always_inline)) {
+    int64_t it = i0 + 16 * t + ul;
+    it = it < n_items ? it : n_items - 1;
+    it = it < 0 ? 0 : it;  // (the deferred loop loads chunk -1 at its start: unused)
+    load_piece<Q>(ei + it * D + gq * Q, af);
+  };
+  auto exact_from = [&](int t, const bool (&gh)[NG], const float (&af)[Q])
+      __attribute__((always_inline)) {
+    const int rel = t * 16 + gq * 4;
+    bool all = true;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) all &= gh[g];
+    f32x4 accs[NG];
+    if (all) {  // every group: the chains interleave on the MFMA pipe
+#pragma unroll
+      for (int g = 0; g < NG; ++g) accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < Q; ++s)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!gh[g]) continue;  // (wave-uniform)
+#pragma unroll
+        for (int s = 0; s < Q; ++s)
+          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (!gh[g]) continue;
+      const f32x4 acc = accs[g];
+      if (__ballot(max4_fresh(acc) > thr[g]) == 0) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = acc[r];
+        const bool cand = rel + r < n_valid && sc > thr[g];
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][pos] = sc;
+            ci[wave][g][ul][pos] = (int)i0 + rel + r;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+  };
+  auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
+    float af[Q];
+    load_exact(t, af);
+    exact_from(t, gh, af);
+  };
+
+  const int lim_end = (int)i1;
+  // tile t: the bf16 screen of its fragments fr, then (rarely) the exact tile and compaction
+  auto screen_tile = [&](int t, const bf16x8 (&fr)[S], auto &&after_mfma)
+      __attribute__((always_inline)) {
+    f32x4 accb[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s], ub[g][s], accb[g], 0, 0, 0);
+    }
+    after_mfma();
+    bool gh[NG];
+    bool hit = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+      hit |= gh[g];
+    }
+    if (hit) {
+      exact_tile(t, gh);
+      const int l = (int)i0 + (t + 1) * 16;
+      maybe_compact(l < lim_end ? l : lim_end);
+    }
+  };
+  if constexpr (SH) {
+    // The block's waves share the bf16 item fragments through LDS: chunks of CI items
+    // (8 KiB, one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a
+    // ring of 3 buffers, chunk c + 2 issued while chunk c is screened; the 16-byte pieces of
+    // row r stored XOR-swizzled by sw(r) through the SOURCE address, so the fragment reads of
+    // any 16 consecutive lanes hit distinct banks (the layout of csrc/gbound.hip). The DMA is
+    // inline asm, invisible to hipcc's waits: each wave waits for its own piece of chunk
+    // c + 1 (vmcnt(1): all but the youngest vector-memory op -- chunk c + 2's piece, or
+    // nothing if the exact path loaded after it) before the barrier that publishes it.
+    constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D, NBUF = 3;
+    static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
+    __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
+    auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
+    const int pp = (int)threadIdx.x, pr = pp / PR;
+    const int pcol = 8 * ((pp % PR) ^ sw(pr));
+    auto dma = [&](int c, int buf) __attribute__((always_inline)) {
+      int64_t it = i0 + (int64_t)c * CI + pr;
+      it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
+      const __bf16 *src = eib + it * D + pcol;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(frs[buf] + 1024 * wave));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    };
+    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform: every wave meets every barrier)
+    // Deferred exact tiles (D <= 64): chunk c's screen only records its hit masks; the fp32
+    // fragments of those tiles are loaded at the start of chunk c + 1 (after its DMA) and the
+    // exact tiles run after chunk c + 1's screen, so their load latency hides behind a
+    // chunk of screening instead of stalling the block at the next barrier. The screen of
+    // chunk c + 1 runs on thresholds one chunk older (lower: more hits, never fewer).
+    constexpr bool DEF = D <= 64;
+    bool pend[TPC][NG];
+#pragma unroll
+    for (int tt = 0; tt < TPC; ++tt)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) pend[tt][g] = false;
+    float afp[DEF ? TPC : 1][Q];
+    auto run_pending = [&](int cp) __attribute__((always_inline)) {
+#pragma unroll
+      for (int tt = 0; tt < TPC; ++tt) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) any |= pend[tt][g];
+        if (!any) continue;
+        const int t = cp * TPC + tt;
+        exact_from(t, pend[tt], afp[DEF ? tt : 0]);
+        const int l = (int)i0 + (t + 1) * 16;
+        maybe_compact(l < lim_end ? l : lim_end);
+      }
+    };
+    dma(0, 0);
+    dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c < n_c; ++c) {
+      dma(c + 2, (c + 2) % NBUF);  // into chunk c - 1's buffer (released by the last barrier)
+      if constexpr (DEF) {  // (only the pending tiles: wave-uniform branches)
+#pragma unroll
+        for (int tt = 0; tt < TPC; ++tt) {
+          bool any = false;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) any |= pend[tt][g];
+          if (any) load_exact((c - 1) * TPC + tt, afp[tt]);
+        }
+      }
+      const char *fb = frs[c % NBUF];
+      bool hm[TPC][NG];
+#pragma unroll
+      for (int tt = 0; tt < TPC; ++tt) {
+        const int t = c * TPC + tt;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) hm[tt][g] = false;
+        if (t >= n_t) continue;
+        bf16x8 fr[S];
+        const int r = 16 * tt + ul;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          fr[s] = *reinterpret_cast<const bf16x8 *>(fb + r * RB + 16 * ((4 * s + gq) ^ sw(r)));
+        f32x4 accb[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < S; ++s)
+            accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s], ub[g][s], accb[g], 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          hm[tt][g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+        if constexpr (!DEF) {
+          bool hit = false;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) hit |= hm[tt][g];
+          if (hit) {
+            exact_tile(t, hm[tt]);
+            const int l = (int)i0 + (t + 1) * 16;
+            maybe_compact(l < lim_end ? l : lim_end);
+          }
+        }
+      }
+      if constexpr (DEF) {
+        run_pending(c - 1);  // (c = 0: nothing pending)
+#pragma unroll
+        for (int tt = 0; tt < TPC; ++tt)
+#pragma unroll
+          for (int g = 0; g < NG; ++g) pend[tt][g] = hm[tt][g];
+      }
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      __syncthreads();
+    }
+    if constexpr (DEF) {  // the last chunk's exact tiles
+#pragma unroll
+      for (int tt = 0; tt < TPC; ++tt) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) any |= pend[tt][g];
+        if (any) load_exact((n_c - 1) * TPC + tt, afp[tt]);
+      }
+      run_pending(n_c - 1);
+    }
+  } else {
+    // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
+    // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
+    // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at
+    // C5, d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
+    bf16x8 fr[2][S];
+    load_bf(0, fr[0]);
+    load_bf(1, fr[1]);
+    for (int t0 = 0; t0 < n_t; t0 += 2) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int t = t0 + p;
+        if (t >= n_t) break;
+        // tile t + 2 into the buffer tile t just left, right after tile t's MFMAs
+        screen_tile(t, fr[p], [&] { load_bf(t + 2, fr[p]); });
+      }
+    }
+  }
+
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t user = ubase + g * 16 + u;
+      if (user >= n_users) break;
+      compact_user(g, u, lim_end);
+      const int nc = __shfl(cnt[g], u);
+      for (int e = lane; e < k; e += 64) {
+        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
+        const int id = e < nc ? ci[wave][g][u][e] : -1;
+        if (n_splits == 1) {
+          out_val[user * k + e] = v;
+          out_idx[user * k + e] = id;
+        } else {
+          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          part_val[o] = v;
+          part_idx[o] = id;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
+template <int M>
+__global__ __launch_bounds__(256) void k_topk_merge(const float *__restrict__ part_val,
+                                                    const int32_t *__restrict__ part_idx,
+                                                    int64_t n_users, int k, int n_splits,
+                                                    float *__restrict__ out_val,
+                                                    int64_t *__restrict__ out_idx) {
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[4][CAP];
+  __shared__ int ci[4][CAP];
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int64_t user = (int64_t)blockIdx.x * 4 + wave;
+  if (user >= n_users) return;
+  int cnt = 0;
+  float tau = neg_inf<float>();
+  int tau_id = kPadId;
+  for (int s = 0; s < n_splits; ++s) {
+    const int64_t base = ((int64_t)s * n_users + user) * k;
+    for (int e0 = 0; e0 < k; e0 += 64) {
+      const int e = e0 + lane;
+      float v = neg_inf<float>();
+      int id = -1;
+      if (e < k) {
+        v = part_val[base + e];
+        id = part_idx[base + e];
+      }
+      const bool cand = id >= 0 && before(v, id, tau, tau_id);
+      const uint64_t bal = __ballot(cand);
+      const int pos = cnt + __popcll(bal & lanemask_lt());
+      if (cand) {
+        cs[wave][pos] = v;
+        ci[wave][pos] = id;
+      }
+      cnt += __popcll(bal);
+      if (cnt > CAP - 64) {
+        wave_sync();
+        cnt = wave_compact<float, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+      }
+    }
+  }
+  wave_sync();
+  const int nc = wave_compact<float, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+  for (int e = lane; e < k; e += 64) {
+    out_val[user * k + e] = e < nc ? cs[wave][e] : neg_inf<float>();
+    out_idx[user * k + e] = e < nc ? ci[wave][e] : -1;
+  }
+}
+
+// Dense masked score tile writer: G[u][i] for a 16-user x 16-item MFMA tile per step.
+template <int D>
+__global__ __launch_bounds__(256) void k_score_dense(
+    const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, float *__restrict__ G,
+    int64_t ldg, int64_t items_per_block) {
+  constexpr int Q = D / 4;
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  // blockIdx.x -> (user group of 64 users = 4 waves x 16, item chunk)
+  const int64_t n_chunks = (n_items + items_per_block - 1) / items_per_block;
+  const int64_t ugrp = blockIdx.x / n_chunks;
+  const int64_t chunk = blockIdx.x % n_chunks;
+  const int64_t u = ugrp * 64 + wave * 16 + ul;
+  const bool uvalid = u < n_users;
+  const int64_t uu = uvalid ? u : n_users - 1;
+  if (ugrp * 64 + wave * 16 >= n_users) return;
+  float uf[Q];
+  load_piece<Q>(eu + uu * D + gq * Q, uf);
+  const int64_t i0 = chunk * items_per_block;
+  int64_t i1 = i0 + items_per_block;
+  if (i1 > n_items) i1 = n_items;
+  // exclusion pointer: this lane's items (it + 4gq + r) increase across tiles
+  int64_t lo = 0, hi = 0;
+  if (ex_rowptr && uvalid) {
+    lo = ex_rowptr[u];
+    hi = ex_rowptr[u + 1];
+    lo = lower_bound_i32(ex_col, lo, hi, (int32_t)i0);
+  }
+  for (int64_t it = i0; it < i1; it += 16) {
+    const int64_t item_l = it + ul;
+    const int64_t itc = item_l < n_items ? item_l : n_items - 1;
+    float af[Q];
+    load_piece<Q>(ei + itc * D + gq * Q, af);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < Q; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[s], acc, 0, 0, 0);
+    if (uvalid) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t item = it + gq * 4 + r;
+      v[r] = acc[r];
+      while (lo < hi && ex_col[lo] < (int32_t)item) ++lo;
+      if (lo < hi && ex_col[lo] == (int32_t)item) v[r] = mask_value;
+    }
+    const int64_t c0 = it + gq * 4;
+    float *row = G + u * ldg;
+    if (c0 + 3 < i1 && ((ldg & 3) == 0)) {
+      *reinterpret_cast<float4 *>(row + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (c0 + r < i1) row[c0 + r] = v[r];
+    }
+    }
+  }
+}
+
+// Measurement knob, compiled in only with -DLG_TOPK_PROBE (make EXTRA=-DLG_TOPK_PROBE):
+// LGCNHS_TOPK_PROBE=1 times the scoring loop with no candidate insertion, =2 drops the
+// exclusion sets. Results are wrong under a probe; the product build always passes 0.
+#ifdef LG_TOPK_PROBE
+static int topk_probe() {
+  const char *e = getenv("LGCNHS_TOPK_PROBE");
+  return e ? atoi(e) : 0;
+}
+#else
+static int topk_probe() { return 0; }
+#endif
+
+template <int D, int NG, int M, int WAVES>
+static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
+                        const int64_t *ex_rowptr, const int32_t *ex_col, float mask_value,
+                        int k, int n_splits, int64_t items_per_split, float *out_val,
+                        int64_t *out_idx, float *part_val, int32_t *part_idx,
+                        hipStream_t stream) {
+  const int64_t users_per_block = (int64_t)WAVES * NG * 16;
+  const int64_t tiles = (n_users + users_per_block - 1) / users_per_block;
+  k_score_topk<D, NG, M, WAVES><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * WAVES), 0,
+                                  stream>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col,
+                                            mask_value, k, n_splits, items_per_split,
+                                            out_val, out_idx, part_val, part_idx,
+                                            topk_probe());
+}
+
+template <int D>
+static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_users,
+                          int64_t n_items, const int64_t *ex_rowptr, const int32_t *ex_col,
+                          float mask_value, int k, int n_splits, int64_t items_per_split,
+                          float *out_val, int64_t *out_idx, float *part_val,
+                          int32_t *part_idx, hipStream_t stream) {
+  // LDS per block: WAVES * NG * 16 * CAP * 8 B = 64 KiB (+256 B per wave) in every
+  // configuration: two blocks per CU.
+  if (M == 1)
+    launch_topk<D, 2, 1, 4>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else if (M == 2)
+    launch_topk<D, 2, 2, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+  else
+    launch_topk<D, 1, 4, 2>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k,
+                            n_splits, items_per_split, out_val, out_idx, part_val, part_idx,
+                            stream);
+}
+
+template <int D>
+static void dispatch_topk_screen(int M, const float *eu, const float *ei, const __bf16 *eub,
+                                 const __bf16 *eib, const float *umarg, int64_t n_users,
+                                 int64_t n_items, const int64_t *ex_rowptr,
+                                 const int32_t *ex_col, float mask_value, int k, int n_splits,
+                                 int64_t items_per_split, float *out_val, int64_t *out_idx,
+                                 float *part_val, int32_t *part_idx, hipStream_t stream) {
+#define LG_SCREEN_LAUNCH(NG, MM, W, SH)                                                        \
+  {                                                                                           \
+    const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
+    const int64_t tiles = (n_users + upb - 1) / upb;                                          \
+    k_score_topk_screen<D, NG, MM, W, SH><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, \
+                                        stream>>>(eu, ei, eub, eib, umarg, n_users, n_items,  \
+                                                  ex_rowptr, ex_col, mask_value, k, n_splits, \
+                                                  items_per_split, out_val, out_idx, part_val, \
+                                                  part_idx);                                  \
+  }
+  // k <= 32: one 8-wave block per CU (128 KiB of lists + the 24 KiB fragment ring) shares
+  // the item fragments; larger lists keep 2-wave blocks that load their own
+  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 8, true)
+  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2, false)
+  else LG_SCREEN_LAUNCH(1, 4, 2, false)
+#undef LG_SCREEN_LAUNCH
+}
+
+static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
+
+static int64_t split_len(int64_t n_items, int n_splits) {
+  int64_t per = (n_items + n_splits - 1) / n_splits;
+  per = (per + 15) / 16 * 16;
+  return per < 16 ? 16 : per;
+}
+
+}  // namespace lg
+
+using namespace lg;
+
+extern "C" size_t lg_score_topk_ws_bytes(int64_t n_users, int64_t n_items, int32_t dim,
+                                         int32_t k, int32_t n_splits) {
+  (void)n_items;
+  (void)dim;
+  if (n_splits <= 1 || n_users <= 0 || k <= 0) return 0;
+  return (size_t)n_splits * (size_t)n_users * (size_t)k * (sizeof(float) + sizeof(int32_t));
+}
+
+extern "C" int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users,
+                                 int64_t n_items, int32_t dim, const int64_t *ex_rowptr,
+                                 const int32_t *ex_col, float mask_value, int32_t k,
+                                 int32_t n_splits, float *out_val, int64_t *out_idx,
+                                 void *ws, size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && out_val && out_idx, "lg_score_topk_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items > 0 && n_items < 0x7fffffff,
+             "lg_score_topk_f32: n_items must be in [1, 2^31-1)");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_topk_f32: dim %d not in {32,64,128}",
+             dim);
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_score_topk_f32: k=%d not in [1,128]", k);
+  LG_REQUIRE(n_splits >= 1 && n_splits <= 4096, "lg_score_topk_f32: bad n_splits %d", n_splits);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_score_topk_f32: ex_rowptr/ex_col must both be set");
+  if (n_users == 0) return LG_OK;
+  const int64_t per = split_len(n_items, n_splits);
+  const int ns = (int)((n_items + per - 1) / per);
+  float *part_val = nullptr;
+  int32_t *part_idx = nullptr;
+  if (ns > 1) {
+    const size_t need = lg_score_topk_ws_bytes(n_users, n_items, dim, k, ns);
+    if (!ws || ws_bytes < need) {
+      set_error("lg_score_topk_f32: workspace %zu < %zu bytes", ws_bytes, need);
+      return LG_ERR_WORKSPACE;
+    }
+    part_val = (float *)ws;
+    part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int M = cap_m(k);
+  if (topk_probe() == 2) ex_rowptr = nullptr, ex_col = nullptr;
+  switch (dim) {
+    case 32: dispatch_topk<32>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    case 64: dispatch_topk<64>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    default: dispatch_topk<128>(M, eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+  }
+  int st = launch_status("lg_score_topk_f32");
+  if (st != LG_OK || ns == 1) return st;
+  const unsigned blocks = (unsigned)((n_users + 3) / 4);
+  if (k <= 64)
+    k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  else
+    k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  return launch_status("lg_score_topk_f32(merge)");
+}
+
+extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, const void *eu_bf16,
+                                          const void *ei_bf16, const float *umarg,
+                                          int64_t n_users, int64_t n_items, int32_t dim,
+                                          const int64_t *ex_rowptr, const int32_t *ex_col,
+                                          float mask_value, int32_t k, int32_t n_splits,
+                                          float *out_val, int64_t *out_idx, void *ws,
+                                          size_t ws_bytes, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && eu_bf16 && ei_bf16 && umarg && out_val && out_idx,
+             "lg_score_topk_screened_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items > 0 && n_items < 0x7fffffff,
+             "lg_score_topk_screened_f32: n_items must be in [1, 2^31-1)");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128,
+             "lg_score_topk_screened_f32: dim %d not in {32,64,128}", dim);
+  LG_REQUIRE(k >= 1 && k <= 128, "lg_score_topk_screened_f32: k=%d not in [1,128]", k);
+  LG_REQUIRE(n_splits >= 1 && n_splits <= 4096, "lg_score_topk_screened_f32: bad n_splits %d",
+             n_splits);
+  LG_REQUIRE(!ex_rowptr == !ex_col,
+             "lg_score_topk_screened_f32: ex_rowptr/ex_col must both be set");
+  LG_REQUIRE(((uintptr_t)eu_bf16 & 15) == 0 && ((uintptr_t)ei_bf16 & 15) == 0,
+             "lg_score_topk_screened_f32: bf16 copies must be 16-byte aligned");
+  if (n_users == 0) return LG_OK;
+  const int64_t per = split_len(n_items, n_splits);
+  const int ns = (int)((n_items + per - 1) / per);
+  float *part_val = nullptr;
+  int32_t *part_idx = nullptr;
+  if (ns > 1) {
+    const size_t need = lg_score_topk_ws_bytes(n_users, n_items, dim, k, ns);
+    if (!ws || ws_bytes < need) {
+      set_error("lg_score_topk_screened_f32: workspace %zu < %zu bytes", ws_bytes, need);
+      return LG_ERR_WORKSPACE;
+    }
+    part_val = (float *)ws;
+    part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int M = cap_m(k);
+  const __bf16 *ub = (const __bf16 *)eu_bf16, *ib = (const __bf16 *)ei_bf16;
+  switch (dim) {
+    case 32: dispatch_topk_screen<32>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    case 64: dispatch_topk_screen<64>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+    default: dispatch_topk_screen<128>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+  }
+  int st = launch_status("lg_score_topk_screened_f32");
+  if (st != LG_OK || ns == 1) return st;
+  const unsigned blocks = (unsigned)((n_users + 3) / 4);
+  if (k <= 64)
+    k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  else
+    k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
+                                                        out_val, out_idx);
+  return launch_status("lg_score_topk_screened_f32(merge)");
+}
+
+extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_users,
+                                  int64_t n_items, int32_t dim, const int64_t *ex_rowptr,
+                                  const int32_t *ex_col, float mask_value, float *G,
+                                  int64_t ldg, lg_stream_t stream) {
+  LG_REQUIRE(eu && ei && G, "lg_score_dense_f32: null pointer");
+  LG_REQUIRE(n_users >= 0 && n_items >= 0 && n_items < 0x7fffffff && ldg >= n_items,
+             "lg_score_dense_f32: bad sizes");
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_dense_f32: dim %d not in {32,64,128}",
+             dim);
+  LG_REQUIRE(!ex_rowptr == !ex_col, "lg_score_dense_f32: ex_rowptr/ex_col must both be set");
+  if (n_users == 0 || n_items == 0) return LG_OK;
+  const int64_t ipb = 1024;
+  const int64_t chunks = (n_items + ipb - 1) / ipb;
+  const int64_t ugrps = (n_users + 63) / 64;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)(ugrps * chunks)), block(256);
+  switch (dim) {
+    case 32: k_score_dense<32><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+    case 64: k_score_dense<64><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+    default: k_score_dense<128><<<grid, block, 0, s>>>(eu, ei, n_users, n_items, ex_rowptr, ex_col, mask_value, G, ldg, ipb); break;
+  }
+  return launch_status("lg_score_dense_f32");
+}
