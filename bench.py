@@ -690,15 +690,35 @@ def launch_ranks(args) -> int | None:
     return subprocess.run(cmd, env=env).returncode
 
 
-def launch_check(world: int, rank: int) -> None:
+def wants_cpu_baseline(rank: int, args) -> bool:
+    """Rank 0 times the CPU baselines at every N (not only N = 1), unless switched off."""
+    return rank == 0 and not args.no_cpu_baseline
+
+
+def launch_check(world: int, rank: int, args) -> None:
     """--launch-check: the rank plumbing alone (process group, one all-reduce, rank 0's
-    JSON line), no GPU work; what the CPU tests drive through launch_ranks()."""
+    JSON line), no GPU work; what the CPU tests drive through launch_ranks(). Rank 0 also
+    runs the propagation CPU baseline on a small CPU graph through the same function and
+    rank rule as the real line, so the N > 1 cpu_baseline field is exercised without a GPU."""
     t = torch.ones(1)
     if world > 1:
         dist.all_reduce(t)
+    cpu = None
+    if wants_cpu_baseline(rank, args):
+        g = torch.Generator().manual_seed(0)  # a small symmetric bipartite CSR, built on CPU
+        U, I = 300, 400
+        keys = torch.unique(torch.randint(0, U, (5000,), generator=g) * I +
+                            torch.randint(0, I, (5000,), generator=g))
+        rows = torch.cat([keys // I, keys % I + U])
+        cols = torch.cat([keys % I + U, keys // I])
+        order = torch.argsort(rows * (U + I) + cols)
+        rows, src = rows[order], cols[order].to(torch.int32)
+        rp = torch.zeros(U + I + 1, dtype=torch.int64)
+        rp[1:] = torch.cumsum(torch.bincount(rows, minlength=U + I), 0)
+        cpu = cpu_baseline(rp, src, U + I, 16, 3, target_nnz=4000, reps=1)
     if rank == 0:
         print(json.dumps({"metric": "launch-check", "n_gpus": world,
-                          "ranks_seen": int(t.item())}), flush=True)
+                          "ranks_seen": int(t.item()), "cpu_baseline": cpu}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -746,7 +766,7 @@ def main():
     if args.launch_check:
         if world > 1:
             dist.init_process_group(args.backend if args.backend != "nccl" else "gloo")
-        launch_check(world, rank)
+        launch_check(world, rank, args)
         return
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -791,7 +811,9 @@ def main():
     dis_l = shard.permute_rows(dis)
     gen = torch.Generator(device=dev).manual_seed(42)
     e0_orig = torch.randn(N, D, device=dev, generator=gen) * 0.1
-    cpu_rp, cpu_src = (rowptr, src) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else (None, None)
+    # the reference's CPU path beside every N's line (north_star: "in the same run"), on rank 0
+    # after the timed region (the other ranks wait at the closing barrier)
+    cpu_rp, cpu_src = (rowptr, src) if wants_cpu_baseline(rank, args) else (None, None)
     train_graph = (rowptr, src) if (world == 1 and not args.no_train) else None
     del rowptr
     if cpu_src is None:

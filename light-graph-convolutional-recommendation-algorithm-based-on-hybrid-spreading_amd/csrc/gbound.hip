@@ -32,22 +32,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBoundMargin = 0.008f;
 
-// max of three floats without the NaN-quieting canonicalisation fmaxf adds (the operands are
-// finite or -inf). Inline asm: hipcc pads no MFMA-result wait states before it, so the
-// caller retires the chunk's MFMAs first (mfma_settle)
+// max of three floats: one v_maximum3_f32 (gfx950), compiler-visible, so hipcc pads the
+// MFMA-result wait states itself (no NaN-quieting canonicalisation as fmaxf would add; the
+// operands are finite or -inf, and a NaN would propagate into the bound)
 __device__ __forceinline__ float max3f(float a, float b, float c) {
-  float m;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
-  return m;
-}
-
-// every MFMA issued above has written its result before any instruction below reads it: no
-// instruction crosses the barriers, and 16 wait states >= the 12 an 8-pass XDL result needs
-// before a VALU read (cdna_hip_programming.md §5.7 item 2)
-__device__ __forceinline__ void mfma_settle() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7");
-  __builtin_amdgcn_sched_barrier(0);
+  return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
 }
 
 __device__ __forceinline__ float round_up_f32(double x) {
@@ -182,7 +171,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
         accs[t][g] = acc;
       }
     }
-    mfma_settle();
     // lane holds rows (items) 4 kg + r of each 16-item tile, column (user) ul; columns past
     // the width (a partial last chunk only) do not count
     if (cb + 64 > width) {
@@ -203,7 +191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       m = max3f(m, accs[2][g][1], accs[2][g][2]);
       m = max3f(m, accs[2][g][3], accs[3][g][0]);
       m = max3f(m, accs[3][g][1], accs[3][g][2]);
-      gmax[g] = fmaxf(m, accs[3][g][3]);
+      gmax[g] = __builtin_elementwise_maximum(m, accs[3][g][3]);
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {

@@ -1298,9 +1298,12 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
             has_qb ? (void *)(a.qb + us * a.qstride) : (void *)a.lines, 0,
             has_qb ? a.qstride : 0, 0x00020000);
+        // (the whole offset in voffset + the immediate, both range-checked against qstride:
+        // a tile narrower than kQPre * 256 columns reads 0 past its row instead of the next
+        // user's -- or, for the last user, past the allocation)
 #pragma unroll
         for (int kk = 0; kk < kQPre; ++kk)
-          st.q[kk] = __builtin_amdgcn_raw_buffer_load_b32(rq, (uint32_t)(4 * lane), 256 * kk, 0);
+          st.q[kk] = __builtin_amdgcn_raw_buffer_load_b32(rq, (uint32_t)(4 * lane + 256 * kk), 0, 0);
       }
       const int32_t nx = x.xh - x.xc;
       const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(

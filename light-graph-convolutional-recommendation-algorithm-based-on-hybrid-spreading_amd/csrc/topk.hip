@@ -43,12 +43,12 @@ __device__ __forceinline__ void load_piece(const float *__restrict__ p, float (&
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-// Item-tile loads: buffer_load through a per-tile descriptor whose base is the tile's first
-// row and whose record count is the bytes left in the table (0 past its end), so rows
+// Item-tile loads: raw buffer loads through a per-tile descriptor whose base is the tile's
+// first row and whose record count is the bytes left in the table (0 past its end), so rows
 // beyond n_items read as 0 and every tile issues the same LT loads with no branch and no
-// per-lane address arithmetic. Inline asm keeps them invisible to the compiler's wait
-// analysis (cdna_hip_programming.md §5.7 item 1); the caller waits by hand with
-// wait_vm<N>() = "all but the N youngest vector-memory ops".
+// per-lane address arithmetic. Compiler-visible (__builtin_amdgcn_raw_buffer_load_b128):
+// hipcc counts these loads itself and places each s_waitcnt vmcnt before the first use.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 template <int D>
 __device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items, int64_t it,
                                                int voff, f32x4v (&v)[D / 16]) {
@@ -59,32 +59,18 @@ __device__ __forceinline__ void load_item_tile(const float *ei, int64_t n_items,
       __builtin_amdgcn_make_buffer_rsrc((void *)(ei + it * D), 0, num, 0x00020000);
 #pragma unroll
   for (int t = 0; t < D / 16; ++t)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3"
-                 : "=v"(v[t])
-                 : "v"(voff), "s"(r), "i"(t * 16)
-                 : "memory");
+    v[t] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * t, 0, 0));
 }
 
-// max of the four scores of an MFMA result (plain v_max3/v_max: the NaN-quieting
-// canonicalisation fmaxf would add is irrelevant for a threshold test). Inline asm: hipcc
-// pads no MFMA-result wait states before it, so it reads only results an MFMA wrote well
-// before (k_score_topk's filter runs one tile behind its MFMAs); right after an MFMA,
-// max4_fresh (compiler-visible: hipcc inserts the wait states).
-__device__ __forceinline__ float max4_fresh(f32x4 a) {
-  return fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
-}
+// max of the four scores of an MFMA result: two v_maximum3_f32 (gfx950), compiler-visible, so
+// hipcc pads the MFMA-result wait states itself. NaN-propagating: callers test
+// !(max4(a) <= thr), which sends a NaN score to the exact per-element test (sc > thr) instead
+// of hiding the tile's other scores behind it.
 __device__ __forceinline__ float max4(f32x4 a) {
-  float m;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a[0]), "v"(a[1]), "v"(a[2]));
-  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(m), "v"(a[3]));
-  return m;
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a[0], a[1]),
+                                       __builtin_elementwise_maximum(a[2], a[3]));
 }
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (§5.4 rule 18)
-}
+__device__ __forceinline__ bool above(float m, float thr) { return !(m <= thr); }
 
 // One wave: NG groups of 16 users; the block's waves work independently.
 //
@@ -95,7 +81,7 @@ __device__ __forceinline__ void wait_vm() {
 //   ->  compact lists that could overflow.
 // The filter's vector instructions fill the MFMA issue gaps (an f32 16x16x4 MFMA holds the
 // SIMD's vector issue for 8 of its 32 cycles), and each tile's loads are in flight for two
-// steps.
+// steps. All loads are compiler-visible: hipcc places the vmcnt waits.
 template <int D, int NG, int M, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const float *__restrict__ eu, const float *__restrict__ ei, int64_t n_users,
@@ -218,7 +204,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
   auto any_cand = [&](const f32x4 (&acc)[NG]) __attribute__((always_inline)) {
     bool any = false;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) any |= max4(acc[g]) > thr[g];
+    for (int g = 0; g < NG; ++g) any |= above(max4(acc[g]), thr[g]);
     return __ballot(any) != 0;
   };
 
@@ -227,7 +213,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (__ballot(max4(acc[g]) > thr[g]) == 0) continue;
+      if (__ballot(above(max4(acc[g]), thr[g])) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float sc = acc[g][r];
@@ -271,20 +257,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     const int l = (int)i0 + (t + 1) * 16;
     return l < lim_end ? l : lim_end;
   };
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the prologue loads: vmcnt(0)
   if (n_t > 0) {
     f32x4v afA[LT], afB[LT];
     f32x4 accA[NG], accB[NG];
     load_item_tile<D>(ei, n_items, i0, voff, afA);
     load_item_tile<D>(ei, n_items, i0 + 16, voff, afB);
-    wait_vm<LT>();
     mfma_tile(afA, accA);
     load_item_tile<D>(ei, n_items, i0 + 32, voff, afA);
     // invariant at step t: acc[t%2] = tile t; buffer (t+1)%2 = tile t+1 (landed or in
     // flight); buffer t%2 = tile t+2 in flight
     for (int t = 0;; t += 2) {
       // ---- even step: tile t in accA, tile t+1 in afB
-      wait_vm<LT>();
       mfma_tile(afB, accB);
       bool hit = any_cand(accA);
       load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 3) * 16, voff, afB);
@@ -292,7 +275,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       maybe_compact(step_lim(t));
       if (t + 1 >= n_t) break;
       // ---- odd step: tile t+1 in accB, tile t+2 in afA
-      wait_vm<LT>();
       mfma_tile(afA, accA);
       hit = any_cand(accB);
       load_item_tile<D>(ei, n_items, i0 + (int64_t)(t + 4) * 16, voff, afA);
@@ -301,7 +283,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
       if (t + 2 >= n_t) break;
     }
   }
-  wait_vm<0>();
 
   // final lists
   wave_sync();
@@ -506,7 +487,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     for (int g = 0; g < NG; ++g) {
       if (!gh[g]) continue;
       const f32x4 acc = accs[g];
-      if (__ballot(max4_fresh(acc) > thr[g]) == 0) continue;
+      if (__ballot(above(max4(acc), thr[g])) == 0) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float sc = acc[r];
@@ -541,7 +522,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     bool hit = false;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      gh[g] = __ballot(max4_fresh(accb[g]) + marg[g] > thr[g]) != 0;
+      // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
+      gh[g] = __ballot(above(max4(accb[g]) + marg[g], thr[g])) != 0;
       hit |= gh[g];
     }
     if (hit) {
@@ -556,8 +538,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     // ring of 3 buffers, chunk c + 2 issued while chunk c is screened; the 16-byte pieces of
     // row r stored XOR-swizzled by sw(r) through the SOURCE address, so the fragment reads of
     // any 16 consecutive lanes hit distinct banks (the layout of csrc/gbound.hip). The DMA is
-    // inline asm, invisible to hipcc's waits: each wave waits for its own piece of chunk
-    // c + 1 (vmcnt(1): all but the youngest vector-memory op -- chunk c + 2's piece, or
+    // inline asm with no register outputs, invisible to hipcc's waits (its own
+    // __builtin_amdgcn_global_load_lds makes hipcc put vmcnt(0) before every LDS read, as it
+    // cannot tell the ring's buffers apart: chunk c + 2's copy would then be waited for before
+    // chunk c is screened). An untracked load only makes hipcc's own vmcnt waits stricter (the
+    // counter retires in order), and each wave waits for its own piece of chunk c + 1
+    // explicitly (vmcnt(1): all but the youngest vector-memory op -- chunk c + 2's piece, or
     // nothing if the exact path loaded after it) before the barrier that publishes it.
     constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D, NBUF = 3;
     static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");

@@ -236,6 +236,8 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     if screen and nu > 0:
         ub, un = bound_operands(eu)
         ib, inorm = bound_operands(ei)
+        # (a non-finite embedding makes a margin NaN or inf: the kernel then recomputes every
+        # tile of those users exactly, so the lists stay lg_score_topk_f32's)
         umarg = un * (inorm.max() * SCREEN_MARGIN)
         N.check(N.lib().lg_score_topk_screened_f32(
             N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d, ex_rp, ex_c,
@@ -756,15 +758,6 @@ def tile_traffic(A: Interactions, tile: int = 2048, users: slice | None = None,
     for j0 in range(i0, i1, tw.tile):
         tw.build(j0, stop=i1)
     return int(tw.paths_read), int(tw.bytes_read)
-
-
-def row_norms(x: torch.Tensor) -> torch.Tensor:
-    """fp64 L2 norm of each row of an fp32 matrix."""
-    x = _f32(x, "x")
-    out = torch.empty(x.shape[0], dtype=torch.float64, device=x.device)
-    N.check(N.lib().lg_row_norms_f64(N.ptr(x), x.shape[0], x.shape[1], N.ptr(out),
-                                     N.stream_handle(x.device)), "lg_row_norms_f64")
-    return out
 
 
 def bound_operands(x: torch.Tensor):

@@ -9,6 +9,7 @@ device->host copy of the [U, k] index matrix.
 from __future__ import annotations
 
 import os
+import zipfile
 
 import numpy as np
 import pandas as pd
@@ -70,6 +71,38 @@ def topk_to_dict(idx: torch.Tensor, n_rows: int | None = None, factory=dict) -> 
     return out
 
 
+def lists_path(path: str) -> str:
+    """The pickle-free sidecar of a saved recommendation dict: '<name>.npy' ->
+    '<name>.lists.npz'."""
+    return (path[:-4] if path.endswith(".npy") else path) + ".lists.npz"
+
+
 def save_recs(recs: dict, path: str) -> None:
+    """The reference's format (np.save of the dict, read back by its evaluationMetrics.py with
+    allow_pickle=True) plus a pickle-free sidecar (lists_path: uids + [U, k] int64 lists,
+    -1 padded) that this package's main.py reads instead, so a cache file is never unpickled
+    here."""
     os.makedirs(os.path.dirname(path), exist_ok=True)
     np.save(path, recs)
+    uids = np.fromiter(recs.keys(), dtype=np.int64, count=len(recs))
+    width = max((len(v) for v in recs.values()), default=0)
+    lists = np.full((len(recs), width), -1, dtype=np.int64)
+    lens = np.zeros(len(recs), dtype=np.int64)
+    for r, v in enumerate(recs.values()):
+        lists[r, :len(v)] = v
+        lens[r] = len(v)
+    np.savez(lists_path(path), uids=uids, lists=lists, lens=lens)
+
+
+# what load_recs raises on a missing, truncated, corrupt or foreign cache file
+CACHE_ERRORS = (OSError, ValueError, KeyError, EOFError, zipfile.BadZipFile)
+
+
+def load_recs(path: str) -> dict:
+    """The dict save_recs wrote, from its pickle-free sidecar only (allow_pickle=False).
+    Raises one of CACHE_ERRORS on a missing, truncated, corrupt or foreign file."""
+    with np.load(lists_path(path), allow_pickle=False) as z:
+        uids, lists, lens = z["uids"], z["lists"], z["lens"]
+    if uids.ndim != 1 or lists.shape[0] != uids.shape[0] or lens.shape != uids.shape:
+        raise ValueError(f"{lists_path(path)}: inconsistent recommendation lists")
+    return {int(u): lists[r, :int(n)].tolist() for r, (u, n) in enumerate(zip(uids, lens))}

@@ -8,10 +8,10 @@ the reference's own ``processing`` package is used if it is importable, otherwis
 error names the CSVs that are expected under ``cfg.PREPROCESSING["save_path"]``."""
 from __future__ import annotations
 
-import numpy as np
 import pandas as pd
 
 from const import cfg
+from lgcnhs.recs import CACHE_ERRORS, load_recs
 from metrics.accurate import getAccurateMetrics
 from metrics.diversity import getDiversityMetrics
 from utils.log import logger
@@ -92,10 +92,12 @@ def main() -> dict:
     try:
         # a dict this package's recommenders saved (lgcnhs.recs.save_recs), as the reference
         # does; the name has no "_" before k, as in reference main.py:62, so (as there) only
-        # LightGCNOpti's saver (no "_" either) hits this cache and the others recompute
-        all_user_recommend_dict = np.load(path, allow_pickle=True).item()
+        # LightGCNOpti's saver (no "_" either) hits this cache and the others recompute. Read
+        # from the saver's pickle-free sidecar (never unpickled); any unreadable, stale or
+        # foreign cache recomputes, as the reference's bare except does (main.py:61-64)
+        all_user_recommend_dict = load_recs(path)
         logger.info("推荐结果读取完毕")
-    except FileNotFoundError:
+    except CACHE_ERRORS:
         logger.info(f"推荐结果读取失败，正在重新进行推荐，选用模型：{name}")
         all_user_recommend_dict = recommend(name, user_num, item_num, rating_df, train_data_df,
                                             val_data_df, test_data_df, user_features_df,

@@ -3,8 +3,9 @@ model/LightGCN/evaluation.py:17-86), called from the periodic-eval block of the 
 loop (reference model/LightGCN/train.py:147-180, here model/LightGCN/train.py).
 
 getValRecommendations scores with the layer-0 embeddings, masks the TRAIN positives only
-with -1024 and takes the top-k (reference :30-52) in one HIP kernel (lg_score_topk_f32;
-ties ordered by (score desc, item asc)); the val adjacency is accepted and unused, as in
+with -1024 and takes the top-k (reference :30-52) in one HIP kernel
+(lg_score_topk_screened_f32, lists bit for bit lg_score_topk_f32's; ties ordered by (score
+desc, item asc)); the val adjacency is accepted and unused, as in
 the reference (it converts it at :38 and never reads it). calValLoss runs the forward on the
 val adjacency (HIP propagation), draws one negative per val edge (structured negative
 sampling, on the device) and returns the BPR loss of those triples rounded to 5 decimals

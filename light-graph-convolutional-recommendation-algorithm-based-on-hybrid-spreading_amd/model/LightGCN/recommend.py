@@ -2,8 +2,10 @@
 (reference model/LightGCN/recommend.py:22-159).
 
 recommendForAllUser scores with the layer-0 embeddings, masks train and val positives with
--1024 and takes the top-k — in one HIP kernel (lg_score_topk_f32) that never holds the
-U x I score matrix; ties are ordered (score desc, item asc).
+-1024 and takes the top-k — in one HIP kernel (lg_score_topk_screened_f32: a bf16 MFMA
+screen, the exact fp32 chain of lg_score_topk_f32 on the tiles it cannot rule out, the same
+lists bit for bit) that never holds the U x I score matrix; ties are ordered (score desc,
+item asc).
 """
 import numpy as np
 import pandas as pd

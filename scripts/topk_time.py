@@ -1,5 +1,8 @@
 """Time ops.score_topk over the C5 catalog (1M items, 32768 users, k=20, e0 ~ N(0, 0.1^2)):
-the bf16-screened kernel against the plain fp32-MFMA one, lists compared bit for bit."""
+the bf16-screened kernel against the plain fp32-MFMA one, lists compared bit for bit.
+  --dims 64,128   embedding widths       --modes screen,plain   kernels
+  --splits auto,1 item splits            --reps 3               timed calls per case"""
+import argparse
 import os
 import sys
 import time
@@ -11,9 +14,17 @@ import torch  # noqa: E402
 from lgcnhs import ops  # noqa: E402
 from lgcnhs.graph import RowSets  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--dims", default="64,128")
+ap.add_argument("--modes", default="screen,plain")
+ap.add_argument("--splits", default="auto,1")
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--users", type=int, default=32768)
+args = ap.parse_args()
+
 dev = torch.device("cuda:0")
-U, I, k = 32768, 1_000_000, 20
-for D in (64, 128):
+U, I, k = args.users, 1_000_000, 20
+for D in [int(x) for x in args.dims.split(",")]:
     g = torch.Generator(device=dev).manual_seed(42)
     eu = torch.randn(U, D, device=dev, generator=g) * 0.1
     ei = torch.randn(I, D, device=dev, generator=g) * 0.1
@@ -21,20 +32,22 @@ for D in (64, 128):
                       torch.randint(0, I, (U * 100,), device=dev, generator=g))
     excl = RowSets.from_pairs(ku // I, ku % I, U, I, dev)
     res = {}
-    for screen in (True, False):
-        for ns in (None, 1):
+    for mode in args.modes.split(","):
+        screen = mode == "screen"
+        for sp in args.splits.split(","):
+            ns = None if sp == "auto" else int(sp)
             ops.score_topk(eu, ei, k, excl, n_splits=ns, screen=screen)
             torch.cuda.synchronize()
             t = time.perf_counter()
-            for _ in range(3):
+            for _ in range(args.reps):
                 v, i = ops.score_topk(eu, ei, k, excl, n_splits=ns, screen=screen)
             torch.cuda.synchronize()
-            dt = (time.perf_counter() - t) / 3
-            res[(screen, ns)] = (v, i)
-            print(f"d={D} screen={screen} splits={ns}: {dt * 1e3:.2f} ms  "
+            dt = (time.perf_counter() - t) / args.reps
+            res[(mode, sp)] = (v, i)
+            print(f"d={D} {mode} splits={sp}: {dt * 1e3:.2f} ms  "
                   f"{U / dt / 1e6:.2f} M users/s  {2 * U * I * D / dt / 1e12:.0f} fp32-equiv TFLOP/s",
                   flush=True)
-    base = res[(False, None)]
+    base = next(iter(res.values()))
     for key, (v, i) in res.items():
         same = torch.equal(i, base[1]) and torch.equal(v.view(torch.int32), base[0].view(torch.int32))
-        print(f"  {key}: identical to plain = {same}", flush=True)
+        print(f"  {key}: identical to {next(iter(res))} = {same}", flush=True)

@@ -29,6 +29,17 @@ def test_gpus_2_launches_two_ranks():
     assert len(lines) == 1, p.stdout  # rank 0 only
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    # rank 0 times the reference's CPU path at N > 1 too (north_star: every N's line)
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert cpu["kind"] == "port" and cpu["unit"] == "edge-layers/s"
+
+
+def test_no_cpu_baseline_flag_drops_it():
+    p = _run(["--gpus", "2", "--backend", "gloo", "--launch-check", "--no-cpu-baseline"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert line["n_gpus"] == 2 and line["cpu_baseline"] is None
 
 
 def test_gpus_1_stays_single_process():

@@ -94,6 +94,24 @@ def test_screened_topk_near_ties_and_wide_norms():
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
+def test_screened_topk_non_finite_rows():
+    """A NaN item row makes every user's screen margin NaN and a NaN user row its own: the
+    screen then recomputes every tile of those users exactly, so the lists stay the plain
+    kernel's bit for bit (NaN scores never enter), and finite items still fill them."""
+    from lgcnhs import ops
+    U, I, d, k = 64, 3000, 64, 20
+    eu, ei = _emb(U, d, 41), _emb(I, d, 42)
+    ei[1234] = float("nan")
+    eu[7] = float("nan")
+    rp, col = _excl(U, I, 0.01, 43)
+    ex = _rowsets(rp, col, U, I)
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, screen=True)
+    v0, i0 = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, screen=False)
+    assert torch.equal(i, i0) and torch.equal(v.view(torch.int32), v0.view(torch.int32))
+    i = i.cpu().numpy()
+    assert (i[np.arange(U) != 7] >= 0).all() and not (i == 1234).any()
+
+
 def test_score_topk_edge_cases():
     from lgcnhs import ops
     # fewer items than k (padding), all-excluded user (mask values surface), ties (equal

@@ -27,3 +27,27 @@ def test_topk_to_dict_large_matches_loop():
     d = topk_to_dict(torch.as_tensor(a))
     for u in range(5000):
         assert d[u] == a[u][a[u] >= 0].tolist()
+
+
+def test_saved_recs_round_trip_without_pickle(tmp_path):
+    """save_recs writes the reference's .npy dict plus a pickle-free sidecar; load_recs (what
+    main.py's Step 2 reads) returns the dict from the sidecar alone, and an unreadable or
+    foreign cache raises one of the errors main.py turns into a recompute."""
+    import pytest
+    from lgcnhs.recs import CACHE_ERRORS, lists_path, load_recs, save_recs
+    recs = {0: [5, 3, 9], 1: [7], 2: [], 3: [0, 1, 2]}
+    path = str(tmp_path / "rec" / "all_user_recommend_dict_HybridS_3.npy")
+    save_recs(recs, path)
+    assert np.load(path, allow_pickle=True).item() == recs  # the reference's format
+    got = load_recs(path)
+    assert got == recs and all(type(x) is int for v in got.values() for x in v)
+    with open(lists_path(path), "wb") as f:  # truncated / corrupt sidecar
+        f.write(b"PK\x03\x04 not a zip")
+    with pytest.raises(CACHE_ERRORS):
+        load_recs(path)
+    # a pickled object array under the sidecar's name is refused, never unpickled
+    np.savez(lists_path(path), uids=np.array([{"x": 1}], dtype=object))
+    with pytest.raises(CACHE_ERRORS):
+        load_recs(path)
+    with pytest.raises(CACHE_ERRORS):
+        load_recs(str(tmp_path / "missing.npy"))

@@ -43,6 +43,15 @@ def test_library_exports_every_symbol():
     assert lib.lg_abi_version() == N.ABI_VERSION
 
 
+def test_integration_table_lists_every_product_export():
+    """INTEGRATION.md §2 names every function of include/lgcnhs.h by its full name."""
+    txt = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    sec = txt[txt.index("## 2. The C ABI"):txt.index("## 3.")]
+    named = set(re.findall(r"`(lg_[a-z0-9_]+)`", sec))
+    missing = [f for f in declared_functions() if f not in named]
+    assert not missing, missing
+
+
 def test_argument_validation_without_gpu():
     from lgcnhs import _native as N
     lib = N.load_library()
