@@ -1206,26 +1206,33 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   if (u_first >= n_users) return;
 
   // row pointers (and exclusion cursor) of the next new user of the stream, prefetched one
-  // user ahead
+  // user ahead. Lane-varying loads (lane 0 / 1: the row's start / end, resp. exclusion cursor /
+  // row end) keep the values in VGPRs until the user starts: a wave-uniform load is read into
+  // SGPRs right away, and hipcc then waits for it where it is issued -- vmcnt(0), draining
+  // every batch line in flight at each new user. Reissued unconditionally at every step
+  // (clamped past the last user; the same address until a user starts): a load issued only
+  // when a user starts leaves a register copy at the join, which hipcc also guards with
+  // vmcnt(0).
   const bool has_ex = MODE == MODE_TOPK && a.ex_rowptr != nullptr;
-  int32_t uq = (int32_t)u_first, bq = (int32_t)a.user_rowptr[u_first],
-          eq = (int32_t)a.user_rowptr[u_first + 1];
-  int32_t xcq = 0, xhq = 0;
-  if (has_ex) {
-    xcq = (int32_t)a.ex_cur[u_first];
-    xhq = (int32_t)a.ex_rowptr[u_first + 1];
-  }
+  int32_t uq = (int32_t)u_first;
+  int32_t pr = 0, px = 0;  // lanes 0, 1: the prefetched (start, end) / (cursor, end)
+  // (positions < 2^31: the low dword of each int64 entry, one 4-byte load -- a whole int64
+  // load's unused high half would pin a register whose reuse hipcc guards with a vmcnt wait)
+  auto pre_load = [&]() __attribute__((always_inline)) {
+    const int64_t uu = uq < n_users ? uq : n_users - 1;
+    pr = reinterpret_cast<const int32_t *>(a.user_rowptr)[2 * (uu + (lane & 1))];
+    if (has_ex) {  // (uniform)
+      const int64_t *p = (lane & 1) ? a.ex_rowptr + uu + 1 : a.ex_cur + uu;
+      px = *reinterpret_cast<const int32_t *>(p);
+    }
+  };
+  pre_load();
   auto new_user = [&]() __attribute__((always_inline)) {
+    const int32_t bq = __builtin_amdgcn_readlane(pr, 0), eq = __builtin_amdgcn_readlane(pr, 1);
+    const int32_t xcq = has_ex ? __builtin_amdgcn_readlane(px, 0) : 0;
+    const int32_t xhq = has_ex ? __builtin_amdgcn_readlane(px, 1) : 0;
     Batch y{uq, bq, bq + kBatchRows < eq ? bq + kBatchRows : eq, eq, true, xcq, xhq};
     uq += (int32_t)G;
-    if (uq < n_users) {
-      bq = (int32_t)a.user_rowptr[uq];
-      eq = (int32_t)a.user_rowptr[uq + 1];
-      if (has_ex) {
-        xcq = (int32_t)a.ex_cur[uq];
-        xhq = (int32_t)a.ex_rowptr[uq + 1];
-      }
-    }
     return y;
   };
   const Batch kEnd{(int32_t)n_users, 0, 0, 0, false, 0, 0};  // past the end of the stream
@@ -1653,14 +1660,17 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   double ra0[Q], ra1[Q];
   UState s0, s1;
   Batch c = new_user();
+  pre_load();
   load_ids(c, it2);
   load_rows(c, it2, w0, ra0);
   load_state(c, s0);
   Batch d = next_batch(c);
+  pre_load();
   load_ids(d, it2);
   load_rows(d, it2, w1, ra1);
   load_state(d, s1);
   Batch n2 = next_batch(d);
+  pre_load();
   load_ids(n2, it2);
   auto step = [&](uint4 (&wc)[Q], double (&rc)[Q], UState &sc) __attribute__((always_inline)) {
     // c's user state (loaded two steps ago) is taken here, where the wait for it counts the
@@ -1681,6 +1691,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
     load_rows(n2, it2, wc, rc);
     load_state(n2, sc);
     const Batch n3 = next_batch(n2);
+    pre_load();
     load_ids(n3, it2);
     c = d;
     d = n2;
