@@ -492,10 +492,10 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, e
         per_user = 2 * k * 16 + st.get("qstride", 0) + 4 * st.get("nch", 0) + 16
         alg = (st["w_bytes"] + 12 * st["user_items"] + per_user * st["users"] * nl) / nl
         ms = st["t_walk_ms"] / nl
-        traffic, traffic_src = (None, {"status": "PMC record is for the 1M-item d=64 walk"})
-        if (U, I) == (1_000_000, 1_000_000) and tile == 2048 and eu.shape[1] == 64:
-            traffic, traffic_src = load_traffic("c5-d64", 1, "spread_tiled.hip",
-                                                "c5-d64/spread_walk")
+        traffic, traffic_src = (None, {"status": "PMC records are for the C5 walks (2048-col tiles)"})
+        if (U, I) == (1_000_000, 1_000_000) and tile == 2048:
+            wl = f"c5-d{int(eu.shape[1])}"
+            traffic, traffic_src = load_traffic(wl, 1, "spread_tiled.hip", f"{wl}/spread_walk")
         gpaths = st["w_paths"] / nl / ms / 1e6
         walk = {"bound": "lds-atomic", "achieved": gpaths, "peak": LDS_F64_ADD_PEAK_G,
                 "unit": "G path-adds/s", "frac": gpaths / LDS_F64_ADD_PEAK_G,
@@ -842,10 +842,14 @@ def main():
         el2, k2, _ = time_propagation(shard, dis_l, e2, d2, L, max(2, args.steps // 2), 1,
                                       world, dev)
         b2 = shard.nnz * (8 + 4 * d2) + shard.n_rows * (4 + 4 * d2)
+        wl2 = args.workload.rsplit("-d", 1)[0] + f"-d{d2}" if "-d" in args.workload else None
+        tr2, tr2_src = load_traffic(wl2, world) if wl2 else (None, {"status": "no record"})
         extra[f"d{d2}"] = {"value": nnz * L * max(2, args.steps // 2) / el2,
                            "unit": "edge-layers/s", "ms_per_step": el2 / max(2, args.steps // 2) * 1e3,
                            "roofline_frac": b2 / k2 / 1e9 / HBM_PEAK_GBS,
-                           "achieved_GBs": b2 / k2 / 1e9}
+                           "achieved_GBs": b2 / k2 / 1e9, "avg_launch_ms": k2 * 1e3,
+                           "alg_bytes_per_launch": b2, "traffic": tr2,
+                           "traffic_source": tr2_src}
         if d2 in args.extra_dim_legs:
             e2o = e2  # original node order (time_propagation permutes its own copy)
             if not args.no_topk:

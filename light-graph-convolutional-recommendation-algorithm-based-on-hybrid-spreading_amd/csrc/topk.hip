@@ -333,7 +333,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
-  constexpr int CAP = 64 * M;
+  // (SH: 48 entries per list -- k + 12 <= 32 held, + 16 per tile -- so the fragment ring gets
+  // the LDS for 7 chunks)
+#ifndef LG_RING_CAP
+#define LG_RING_CAP 48
+#endif
+  constexpr int CAP = SH ? LG_RING_CAP : 64 * M;
+  static_assert(!SH || M == 1, "the shared-fragment kernel is the k <= 32 one");
   __shared__ float cs[WAVES][NG][16][CAP];
   __shared__ int ci[WAVES][NG][16][CAP];
   __shared__ int exs[WAVES][64];
@@ -549,42 +555,82 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     }
   };
   if constexpr (SH) {
-    // The block's waves share the bf16 item fragments through LDS: chunks of CI items
-    // (8 KiB, one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a
-    // ring of 3 buffers, chunk c + 2 issued while chunk c is screened; the 16-byte pieces of
-    // row r stored XOR-swizzled by sw(r) through the SOURCE address, so the fragment reads of
-    // any 16 consecutive lanes hit distinct banks (the layout of csrc/gbound.hip). The DMA is
-    // inline asm with no register outputs, invisible to hipcc's waits (its own
-    // __builtin_amdgcn_global_load_lds makes hipcc put vmcnt(0) before every LDS read, as it
-    // cannot tell the ring's buffers apart: chunk c + 2's copy would then be waited for before
-    // chunk c is screened). An untracked load only makes hipcc's own vmcnt waits stricter (the
-    // counter retires in order), and each wave waits for its own piece of chunk c + 1
-    // explicitly (vmcnt(1): all but the youngest vector-memory op -- chunk c + 2's piece, or
-    // nothing if the exact path loaded after it) before the barrier that publishes it.
-    constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D, NBUF = 3;
+    // The block's waves share the bf16 item fragments through LDS: chunks of CI items (8 KiB,
+    // one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a ring of
+    // NBUF buffers; the 16-byte pieces of row r stored XOR-swizzled by sw(r) through the
+    // SOURCE address, so the fragment reads of any 16 consecutive lanes hit distinct banks
+    // (the layout of csrc/gbound.hip).
+    // No block barrier per chunk: an exact tile (a global load round trip, the fp32 chain, the
+    // insertion) holds one wave for several chunks' worth of screening, and a barrier made
+    // every wave wait for the slowest one each chunk. Instead the waves drift up to 2 chunks
+    // apart, coupled by two LDS counters per buffer:
+    //   arrive[b]: +1 per wave once its piece of the chunk in b has landed (its own vmcnt);
+    //   done[b]:   +1 per wave once it has read the chunk in b.
+    // Wave w at chunk c: (1) once every wave is done with chunk c + LA - NBUF, issue its piece
+    // of chunk c + LA into that buffer; (2) vmcnt(LAG) -- its pieces up to chunk c + LA - LAG
+    // have landed -- and signal arrival for chunk c + LA - LAG; (3) wait until all WAVES
+    // pieces of chunk c have arrived; (4) screen it; (5) signal done. The slowest wave never
+    // waits (the others are past the chunks it needs them for), so the ring cannot deadlock; a
+    // wave is at most min(LA - LAG, NBUF - LA) chunks ahead of the slowest. The DMA is inline asm with no register
+    // outputs, invisible to hipcc's waits (hipcc's own __builtin_amdgcn_global_load_lds puts
+    // vmcnt(0) before every LDS read, as it cannot tell the ring's buffers apart); an
+    // untracked load only makes hipcc's own vmcnt waits stricter (the counter retires in
+    // order).
+    constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D;
+#ifndef LG_RING_NBUF  // (measurement builds may override the ring shape: -DLG_RING_NBUF=...)
+#define LG_RING_NBUF 7
+#define LG_RING_LA 4
+#define LG_RING_LAG 2
+#endif
+    // ring buffers; chunks a wave issues ahead of its own; chunks between a piece's issue and
+    // its arrival signal
+    constexpr int NBUF = LG_RING_NBUF, LA = LG_RING_LA, LAG = LG_RING_LAG;
     static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
+    static_assert(LAG >= 1 && LA > LAG && NBUF > LA, "ring shape");
     __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
+    __shared__ uint32_t arrive[NBUF], done[NBUF];
     auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
     const int pp = (int)threadIdx.x, pr = pp / PR;
     const int pcol = 8 * ((pp % PR) ^ sw(pr));
-    auto dma = [&](int c, int buf) __attribute__((always_inline)) {
+    auto dma = [&](int c) __attribute__((always_inline)) {
       int64_t it = i0 + (int64_t)c * CI + pr;
       it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
       const __bf16 *src = eib + it * D + pcol;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(frs[buf] + 1024 * wave));
+      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(
+          __attribute__((address_space(3))) char *)(frs[c % NBUF] + 1024 * wave));
       uint32_t keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                    "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
     };
-    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform: every wave meets every barrier)
-    dma(0, 0);
-    dma(1, 1);
-    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    __syncthreads();
+    // the counters are monotone: chunk c is the (c / NBUF + 1)-th generation of buffer c % NBUF
+    auto signal = [&](uint32_t *ctr) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wave's reads are complete)
+      if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_for = [&](uint32_t *ctr, uint32_t target) __attribute__((always_inline)) {
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+        __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    };
+    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform)
+    if (threadIdx.x < NBUF) {
+      arrive[threadIdx.x] = 0u;
+      done[threadIdx.x] = 0u;
+    }
+    __syncthreads();  // (the only block barrier)
+    for (int c = 0; c < LA; ++c) dma(c);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG) : "memory");
+    for (int c = 0; c < LA - LAG; ++c) signal(&arrive[c]);
     for (int c = 0; c < n_c; ++c) {
-      dma(c + 2, (c + 2) % NBUF);  // into chunk c - 1's buffer (released by the last barrier)
+      {
+        const int cn = c + LA, cp = cn - NBUF;  // chunk cn replaces chunk cp in its buffer
+        if (cp >= 0) wait_for(&done[cp % NBUF], (uint32_t)(WAVES * (cp / NBUF + 1)));
+        dma(cn);  // (chunks past the split: harmless clamped reads, signalled like the rest)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG) : "memory");
+        signal(&arrive[(cn - LAG) % NBUF]);
+      }
+      wait_for(&arrive[c % NBUF], (uint32_t)(WAVES * (c / NBUF + 1)));
       const char *fb = frs[c % NBUF];
       const int t0 = c * TPC;
       // The chunk's TPC tiles are screened together -- every fragment read, then every bf16
@@ -593,7 +639,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       // the thresholds of the chunk start: never above the running ones (they only rise), so
       // a tile they rule out holds no score that could enter later either. (Deferring the
       // exact tiles by one chunk, so their fp32 loads overlap the next chunk's screen, was
-      // measured slower: 20.7 vs 17.9 ms at C5, d = 64.)
+      // measured slower: 20.7 vs 17.9 ms at C5, d = 64, with a barrier per chunk.)
       bf16x8 fr[TPC][S];
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt) {
@@ -614,6 +660,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
             accb[tt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[tt][s], ub[g][s],
                                                                   accb[tt][g], 0, 0, 0);
         }
+      signal(&done[c % NBUF]);  // (the fragments are in registers: the buffer is free)
       uint32_t hits = 0;  // bit tt * NG + g: group g's screen hit in tile tt (wave-uniform)
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt)
@@ -632,9 +679,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
         const int l = (int)i0 + (t0 + tt + 1) * 16;
         maybe_compact(l < lim_end ? l : lim_end);
       }
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA in flight at the exit)
   } else {
     // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
     // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
