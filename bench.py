@@ -628,8 +628,49 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
                            "tflops_per_gpu": flops / tp / 1e12,
                            "mfma_frac": flops / tp / 1e12 / F32_MFMA_PEAK_TF,
                            "kernel": "lg_score_topk_f32 (f32 MFMA 16x16x4 + streaming top-k)"}}
+    line["roofline"] = topk_roofline(nu, I, D, k, tk)
     lists = ops.score_topk(eu, ei, k, excl)[1] if u0 == 0 else None
     return line, lists
+
+
+def topk_roofline(nu, I, D, k, tk):
+    """roofline of the screened top-K kernel (MFMA-bound): the MFMA work it executes -- the bf16
+    screen of every (user, item) and the exact fp32 chain of the (16-user group, 16-item tile)
+    pairs the screen cannot rule out -- priced in bf16-equivalent TFLOP/s (an fp32 MFMA flop
+    takes 2500 / 157.3 bf16 flops' worth of MFMA-pipe time) against the dense bf16 peak, so frac
+    is the MFMA pipe's busy fraction implied by the live time. The exact share, the PMC
+    MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES) and the HBM traffic come from
+    profiles/pmc_topk.json (scripts/gpu_r04_topk.sh + scripts/topk_pmc_summary.py), used only
+    if recorded on this csrc/topk.hip at this shape; without one, achieved counts the screen
+    alone (a lower bound) and says so."""
+    import hashlib
+    sha = hashlib.sha256(open(os.path.join(PKG, "csrc", "topk.hip"), "rb").read()).hexdigest()[:16]
+    rec, status = None, f"no PMC record for c5-d{D}/topk"
+    try:
+        rec = json.load(open(os.path.join(REPO, "profiles", "pmc_topk.json"))).get(f"c5-d{D}/topk")
+    except Exception:
+        rec = None
+    if rec is not None:
+        if rec.get("kernel_sha") != sha:
+            rec, status = None, "stale: recorded on another topk.hip"
+        elif (rec.get("users"), rec.get("items"), rec.get("k")) != (nu, I, k):
+            rec, status = None, "recorded at another shape"
+        else:
+            status = "measured"
+    bf16 = 2.0 * nu * I * D
+    share = rec["exact_group_tile_share"] if rec else None
+    f32 = bf16 * share if share is not None else 0.0
+    achieved = (bf16 + f32 * BF16_MFMA_PEAK_TF / F32_MFMA_PEAK_TF) / tk / 1e12
+    return {"bound": "mfma", "achieved": achieved, "peak": BF16_MFMA_PEAK_TF,
+            "unit": "TFLOP/s (bf16-equivalent MFMA work)", "frac": achieved / BF16_MFMA_PEAK_TF,
+            "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+            "kernel": "lg_score_topk_screened_f32", "avg_launch_ms": tk * 1e3,
+            "exact_group_tile_share": share,
+            "pmc_mfma_busy_frac": rec.get("mfma_busy_frac") if rec else None,
+            "pmc_avg_ms": rec.get("avg_ms") if rec else None,
+            "pmc_wave_parked_frac": rec.get("wave_parked_frac") if rec else None,
+            "record_source": {"status": status, "kernel_sha": sha,
+                              "source": rec.get("source") if rec else None}}
 
 
 def load_traffic(workload, world, src_name="spmm.hip", key=None):

@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 10
+#define LG_ABI_VERSION 11
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -325,7 +325,9 @@ int lg_topk_lists_merge_f64(const double *in_val, const int64_t *in_idx, int32_t
  * ex_col, ...) and advanced here. Walked over tiles in ascending order, the lists equal
  * lg_rows_topk_f64 over the F rows the walk sums. k in [1, 128]; dim in
  * {32, 64, 128}. The walk keeps its stream positions in 32 bits: n_users, the interactions
- * (user_rowptr[n_users]) and the exclusions (ex_rowptr[n_users]) must each be < 2^31.
+ * and the exclusions must each be < 2^31; n_positions / n_ex_positions are upper bounds of
+ * user_rowptr[n_users] / ex_rowptr[n_users] (the lengths of user_items / ex_col, 0 without
+ * exclusions), checked here -- the library does not read device memory on the host.
  * lg_spread_tile_resource_topk_lds_bytes: LDS of one wave plus the
  * workgroup's tables (the launch fits as many waves per CU as the LDS holds). */
 size_t lg_spread_tile_resource_topk_lds_bytes(int32_t tile, int32_t k, int32_t dim);
@@ -339,7 +341,8 @@ int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *
                                      const uint8_t *qb, int32_t qstride,
                                      const int64_t *ex_rowptr, const int32_t *ex_col,
                                      int64_t *ex_cur, int32_t k, int32_t first,
-                                     double *io_val, int64_t *io_idx, lg_stream_t stream);
+                                     double *io_val, int64_t *io_idx, int64_t n_positions,
+                                     int64_t n_ex_positions, lg_stream_t stream);
 
 /* x_bf16[r] = bf16(x[r]) (round to nearest even), norm_up[r] = ||x[r]||_2 rounded up to
  * fp32: the operands of lg_score_chunk_bound (csrc/gbound.hip). */

@@ -2147,10 +2147,15 @@ extern "C" int lg_spread_tile_resource_topk_f64(
     const float *ei, int32_t dim, const float *gb, int32_t n_chunks, const uint8_t *qb,
     int32_t qstride, const int64_t *ex_rowptr,
     const int32_t *ex_col, int64_t *ex_cur, int32_t k, int32_t first, double *io_val,
-    int64_t *io_idx, lg_stream_t stream) {
+    int64_t *io_idx, int64_t n_positions, int64_t n_ex_positions, lg_stream_t stream) {
   LG_REQUIRE(user_rowptr && user_items && ra_edge && lines && ovf && rbeta && inv_cls &&
                  io_val && io_idx && n_users >= 0 && n_users < 0x7fffffff && item_begin >= 0,
              "lg_spread_tile_resource_topk_f64: bad arguments");
+  // (the walk's stream positions are 32-bit)
+  LG_REQUIRE(n_positions >= 0 && n_positions < 0x7fffffff && n_ex_positions >= 0 &&
+                 n_ex_positions < 0x7fffffff,
+             "lg_spread_tile_resource_topk_f64: %lld interactions / %lld exclusions exceed the "
+             "walk's 32-bit positions", (long long)n_positions, (long long)n_ex_positions);
   LG_REQUIRE(tile >= 1 && tile <= 8192 && width >= 1 && width <= tile &&
                  (int64_t)item_begin + width < 0x7fffffff,
              "lg_spread_tile_resource_topk_f64: tile %d / width %d", tile, width);

@@ -669,15 +669,38 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
           // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
           if (__ballot(above(max4(accb[tt][g]) + marg[g], thr[g])) != 0 && t0 + tt < n_t)
             hits |= 1u << (tt * NG + g);
-      while (hits) {
-        const int tt = (__builtin_ctz(hits)) / NG;
-        bool gh[NG];
+#ifndef LG_EXACT_BATCH
+#define LG_EXACT_BATCH 1
+#endif
+      if constexpr (LG_EXACT_BATCH && D <= 64) {
+        // the fp32 fragments of every hit tile of the chunk are loaded together (one load
+        // round trip for the chunk's exact tiles: all of them while the thresholds warm up),
+        // then the tiles run in order
+        float afc[TPC][Q];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) gh[g] = (hits >> (tt * NG + g)) & 1u;
-        hits &= ~(((1u << NG) - 1u) << (tt * NG));
-        exact_tile(t0 + tt, gh);
-        const int l = (int)i0 + (t0 + tt + 1) * 16;
-        maybe_compact(l < lim_end ? l : lim_end);
+        for (int tt = 0; tt < TPC; ++tt)
+          if ((hits >> (tt * NG)) & ((1u << NG) - 1u)) load_exact(t0 + tt, afc[tt]);
+#pragma unroll
+        for (int tt = 0; tt < TPC; ++tt) {
+          if (((hits >> (tt * NG)) & ((1u << NG) - 1u)) == 0) continue;  // (wave-uniform)
+          bool gh[NG];
+#pragma unroll
+          for (int g = 0; g < NG; ++g) gh[g] = (hits >> (tt * NG + g)) & 1u;
+          exact_from(t0 + tt, gh, afc[tt]);
+          const int l = (int)i0 + (t0 + tt + 1) * 16;
+          maybe_compact(l < lim_end ? l : lim_end);
+        }
+      } else {
+        while (hits) {
+          const int tt = (__builtin_ctz(hits)) / NG;
+          bool gh[NG];
+#pragma unroll
+          for (int g = 0; g < NG; ++g) gh[g] = (hits >> (tt * NG + g)) & 1u;
+          hits &= ~(((1u << NG) - 1u) << (tt * NG));
+          exact_tile(t0 + tt, gh);
+          const int l = (int)i0 + (t0 + tt + 1) * 16;
+          maybe_compact(l < lim_end ? l : lim_end);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA in flight at the exit)

@@ -865,7 +865,8 @@ class TileWalk:
             N.ptr(q), 0 if q is None else q.shape[1],
             N.ptr(ex.rowptr if ex is not None else None),
             N.ptr(ex.col if ex is not None else None), N.ptr(self.ex_cur), self.k,
-            int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), N.stream_handle(self.dev)),
+            int(bool(first)), N.ptr(self.vals), N.ptr(self.idxs), A.by_user.col.numel(),
+            ex.col.numel() if ex is not None else 0, N.stream_handle(self.dev)),
             "lg_spread_tile_resource_topk_f64")
 
 

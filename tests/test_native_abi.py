@@ -71,6 +71,13 @@ def test_argument_validation_without_gpu():
     assert st == 1 and b"live" in lib.lg_last_error()
     st = lib.lg_spmm_layer_live_f32(one, one, one, z, one, z, z, z, z, 10, 0, 48, 0, 1.0, 0, one, z)
     assert st == 1 and b"lg_spmm_layer_live_f32" in lib.lg_last_error()
+    # the walk's 32-bit stream positions: the caller's bounds are checked before any launch
+    args = [one, one, one, 10, one, one, 5, one, one, 0, 2048, 2048, z, z, 0, z, 0, z, 0,
+            z, z, z, 20, 1, one, one]
+    st = lib.lg_spread_tile_resource_topk_f64(*args, 2**31, 0, z)
+    assert st == 1 and b"32-bit positions" in lib.lg_last_error()
+    st = lib.lg_spread_tile_resource_topk_f64(*args, 1000, 2**33, z)
+    assert st == 1 and b"32-bit positions" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
 
