@@ -562,7 +562,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     // (the layout of csrc/gbound.hip).
     // No block barrier per chunk: an exact tile (a global load round trip, the fp32 chain, the
     // insertion) holds one wave for several chunks' worth of screening, and a barrier made
-    // every wave wait for the slowest one each chunk. Instead the waves drift up to 2 chunks
+    // every wave wait for the slowest one each chunk. Instead the waves drift up to 3 chunks
     // apart, coupled by two LDS counters per buffer:
     //   arrive[b]: +1 per wave once its piece of the chunk in b has landed (its own vmcnt);
     //   done[b]:   +1 per wave once it has read the chunk in b.
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
 #ifndef LG_RING_NBUF  // (measurement builds may override the ring shape: -DLG_RING_NBUF=...)
 #define LG_RING_NBUF 7
 #define LG_RING_LA 4
-#define LG_RING_LAG 2
+#define LG_RING_LAG 1
 #endif
     // ring buffers; chunks a wave issues ahead of its own; chunks between a piece's issue and
     // its arrival signal
@@ -669,8 +669,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
           // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
           if (__ballot(above(max4(accb[tt][g]) + marg[g], thr[g])) != 0 && t0 + tt < n_t)
             hits |= 1u << (tt * NG + g);
-#ifndef LG_EXACT_BATCH
-#define LG_EXACT_BATCH 1
+#ifdef LG_SCREEN_PROBE  // measurement builds only (wrong lists): 1 = screen alone, 2 = all exact
+      hits = LG_SCREEN_PROBE == 1 ? 0u : (t0 + TPC <= n_t ? (1u << (TPC * NG)) - 1u : hits);
+#endif
+#ifndef LG_EXACT_BATCH  // (1: measured slower, 15.0 vs 13.9 ms at C5, d = 64)
+#define LG_EXACT_BATCH 0
 #endif
       if constexpr (LG_EXACT_BATCH && D <= 64) {
         // the fp32 fragments of every hit tile of the chunk are loaded together (one load
