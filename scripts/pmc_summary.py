@@ -80,4 +80,6 @@ def main(out_dir, tag, workload="c5-d64", world=1):
 
 
 if __name__ == "__main__":
-    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r02")
+    # usage: pmc_summary.py TAG [WORKLOAD (c5-d64)]
+    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r02",
+         sys.argv[2] if len(sys.argv) > 2 else "c5-d64")
