@@ -79,7 +79,7 @@ def test_argument_validation_without_gpu():
     st = lib.lg_spread_tile_resource_topk_f64(*args, 1000, 2**33, z)
     assert st == 1 and b"32-bit positions" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
-    assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * (10 * 8 + 4)
+    assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
 
 
 def test_missing_library_fails_loudly(tmp_path):
