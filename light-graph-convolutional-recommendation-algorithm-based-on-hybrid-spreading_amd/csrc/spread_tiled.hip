@@ -1323,6 +1323,15 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   // ---- decode one batch into acc
   auto decode = [&](const Batch &x, uint4 (&w)[Q], const double (&ra)[Q])
       __attribute__((always_inline)) {
+#ifdef LG_WALK_PROBE  // measurement builds only (wrong lists): 2 = no decode (lines loaded only)
+    if (LG_WALK_PROBE == 2) {
+      uint32_t h = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) h ^= w[q].x ^ w[q].y ^ w[q].z ^ w[q].w ^ (uint32_t)ra[q];
+      if (h == 0x12345678u && lane == 64) acc[0] = 1.0;  // (keeps the loads; never true)
+      return;
+    }
+#endif
     uint32_t hdr = 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) hdr |= w[q].x & ~hmask;  // the group heads' headers
@@ -1407,6 +1416,14 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   auto finish_user = [&](const Batch &x, UState &st) __attribute__((always_inline)) {
     const int64_t u = x.u;
     wave_sync();
+#ifdef LG_WALK_PROBE  // measurement builds only (wrong lists): 1 = no scan (acc zeroed only)
+    if (LG_WALK_PROBE == 1) {
+      for (int j = 2 * lane; j < acc_cols(tile); j += 128)
+        *reinterpret_cast<double2 *>(acc + j) = double2{0.0, 0.0};
+      wave_sync();
+      return;
+    }
+#endif
     if constexpr (MODE == MODE_F) {
       double *row = a.F + u * a.ldf;
       for (int j = lane; j < tile; j += 64) {
