@@ -39,6 +39,21 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
   return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
 }
 
+// max of a value over the lanes l, l ^ 16, l ^ 32, l ^ 48 (the four 16-lane rows) by the
+// gfx950 row swaps (VALU; a __shfl_xor is an LDS-pipe ds_bpermute and a wait per step). Inline
+// asm: hipcc's __builtin_amdgcn_permlane{16,32}_swap returns the swapped vdst as both halves of
+// its result (the second register is lost -- seen in the ISA of a two-output test kernel). The
+// nops cover the VALU-write -> permlane read and permlane -> VALU read hazards.
+__device__ __forceinline__ float row_max4(float m) {
+  uint32_t x = __builtin_bit_cast(uint32_t, m), y = x;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  m = fmaxf(__builtin_bit_cast(float, x), __builtin_bit_cast(float, y));
+  x = __builtin_bit_cast(uint32_t, m);
+  y = x;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+  return fmaxf(__builtin_bit_cast(float, x), __builtin_bit_cast(float, y));
+}
+
 __device__ __forceinline__ float round_up_f32(double x) {
   float f = (float)x;
   if ((double)f < x) f = nextafterf(f, __builtin_huge_valf());
@@ -135,23 +150,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   const __amdgpu_buffer_rsrc_t rgb = __builtin_amdgcn_make_buffer_rsrc(
       (void *)(gb + (ubase < n_users ? ubase : 0) * nch), 0,
       nrow_w > 0 ? (int)(nrow_w * nch * 4) : 0, 0x00020000);
+  // every chunk's largest item norm (the margin's ||j|| factor), once per block: wave w folds
+  // chunks w, w + 4, ... (the loads first, then the reductions side by side)
+  __shared__ float s_cmax[64];
+  {
+    constexpr int CPW = 16;  // chunks per wave (nch <= 64)
+    float v[CPW];
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) {
+      const int j = 64 * (wv + 4 * k) + lane;
+      v[k] = j < width ? inorm[item_begin + j] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) {
+      if (64 * (wv + 4 * k) >= width) break;
+      float m = row_max4(v[k]);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if (lane == 0) s_cmax[wv + 4 * k] = m;
+    }
+  }
   dma(0, 0);
-  float na = lane < width ? inorm[item_begin + lane] : 0.f;
   // the DMA is inline asm, invisible to hipcc's waits: this wave's copies have landed only
-  // after an explicit vmcnt(0), which must precede the barrier that publishes the buffer
+  // after an explicit vmcnt wait, which must precede the barrier that publishes the buffer
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // every prologue load (the user fragments and norms above) is taken here, before the loop:
+  // a load still pending at the loop head gets its wait inside the loop, where it also drains
+  // the next chunk's DMA in every iteration
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) asm volatile("" : "+v"(bfr[g][s]));
+    asm volatile("" : "+v"(un[g]));
+  }
   for (int c = 0; c < nch; ++c) {
     const int cb = 64 * c;  // chunk start inside the tile
-    float nb = 0.f;
-    if (c + 1 < nch) {
+    if (c + 1 < nch)
       dma(cb + 64, (c + 1) & 1);  // into the buffer every wave finished reading at the last barrier
-      nb = cb + 64 + lane < width ? inorm[item_begin + cb + 64 + lane] : 0.f;
-    }
-    // the chunk's largest item norm (wave-uniform)
-    float inm = na;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) inm = fmaxf(inm, __shfl_xor(inm, o));
+    const float inm = s_cmax[c];  // the chunk's largest item norm
     float gmax[4];
     f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
@@ -195,15 +232,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      float m = gmax[g];
-      m = fmaxf(m, __shfl_xor(m, 16));
-      m = fmaxf(m, __shfl_xor(m, 32));
+      const float m = row_max4(gmax[g]);
       const float marg = kBoundMargin * un[g] * inm;
       float b = m + marg;
       b += fabsf(b) * 0x1p-22f + 1e-30f;
-      if (kg == 0)  // (rows past n_users: out of the descriptor's range, dropped)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, b), rgb,
-                                              (uint32_t)(4 * ((16 * g + ul) * nch + c)), 0, 0);
+      // every lane stores (one store per wave and group, not a branch that hipcc's waits
+      // would have to count as possibly skipped): lanes kg > 0 and rows past n_users fall
+      // outside the descriptor's range and are dropped
+      __builtin_amdgcn_raw_buffer_store_b32(
+          __builtin_bit_cast(uint32_t, b), rgb,
+          kg == 0 ? (uint32_t)(4 * ((16 * g + ul) * nch + c)) : 0x7FFFFFF0u, 0, 0);
       if (qb) {
         // per column: q = rne(v') with v' = fl(acc sc + msc) >= 255 (acc + marg) / b + 0.5 (sc
         // and msc carry (1 + 2^-20) factors over their own roundings and the fma's; msc holds
@@ -228,7 +266,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
         }
       }
     }
-    if (qb && ((c & 1) || c + 1 == nch)) {  // a chunk pair is complete: write it out
+    const bool pair = qb && ((c & 1) || c + 1 == nch);
+    if (pair) {  // a chunk pair is complete: write it out
       wave_sync();
       const int cp = 64 * (c & ~1);  // the pair's first column (its 128 columns fit qstride)
       // the wave's 64 q rows through one descriptor (rows past n_users are out of range:
@@ -242,15 +281,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
         const int uloc = 8 * r8 + (lane >> 3);
         const uint4 v =
             *reinterpret_cast<const uint4 *>(qs + uloc * QS + 4 * ((lane & 7) ^ (uloc & 7)));
+#ifdef LG_QBLOCKED  // measurement: the wave's 64 rows of a chunk pair as one 8 KB block
+        const uint32_t qo = (uint32_t)((cp / 128) * nrow * 128 + uloc * 128 + 16 * (lane & 7));
+#else
+        const uint32_t qo = (uint32_t)(uloc * qstride + cp + 16 * (lane & 7));
+#endif
         __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rq,
-            (uint32_t)(uloc * qstride + cp + 16 * (lane & 7)), 0, 0);
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rq, qo, 0, 0);
       }
       wave_sync();
     }
-    na = nb;
-    // chunk c + 1's DMA (this wave's share) landed, then the barrier publishes the buffer
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // chunk c + 1's DMA (this wave's share) landed, then the barrier publishes the buffer.
+    // vmcnt counts stores as well, and completes in issue order: the wait leaves this chunk's
+    // 4 gb stores and the pair's 8 q stores (issued after the DMA, no loads in the loop) in
+    // flight -- a vmcnt(0) here would wait for every store to reach L2 once per chunk
+    if (pair)
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __syncthreads();
   }
 }

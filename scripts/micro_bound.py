@@ -57,6 +57,10 @@ def fill(r=0):
 
 res = {"users": a.users, "tile": T, "dim": a.dim,
        "with_q_ms": timed(with_q), "gb_only_ms": timed(gb_only), "fill_q_ms": timed(fill)}
+with_q(0)  # bitwise fingerprint of one tile's bounds (A/B builds must agree)
+torch.cuda.synchronize()
+res["q_sum"] = int(q.to(torch.int64).sum())
+res["gb_bits_sum"] = int(gb.view(torch.int32).to(torch.int64).sum())
 qbytes = a.users * T
 res["fill_GBps"] = qbytes / res["fill_q_ms"] / 1e6
 res["with_q_write_GBps"] = (qbytes + gb.numel() * 4) / res["with_q_ms"] / 1e6
