@@ -1522,6 +1522,15 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
       double *cq_f = ovl_ra;     // queued f (the decode's overflow list, free during the scan)
       uint32_t *cq_j = ovl_ent;  // queued column
       auto flush = [&]() __attribute__((always_inline)) {
+#ifdef LG_WALK_PROBE  // 3 = no exact scores: candidates inserted with their f as the score
+        if (LG_WALK_PROBE == 3) {
+          wave_sync();
+          for (int mm = 0; mm < ncand; ++mm) insert1(cq_f[mm], a.item_begin + (int)cq_j[mm]);
+          ncand = 0;
+          wave_sync();
+          return;
+        }
+#endif
         if constexpr (D > 0) {
           constexpr int Qd = D / 4;              // MFMA steps
           constexpr int H = Qd < 16 ? Qd : 16;   // steps per load round (<= 16 VGPRs each)
