@@ -657,9 +657,12 @@ def topk_roofline(nu, I, D, k, tk):
             rec, status = None, "recorded at another shape"
         else:
             status = "measured"
-    bf16 = 2.0 * nu * I * D
+    # (k <= 32 on a catalog of >= 1024 k items: the seed pass screens the first 1/16 of the
+    # items once more, csrc/topk.hip)
+    seeded = k <= 32 and I // 16 // 16 * 16 >= 64 * k
+    bf16 = 2.0 * nu * I * D * (1.0 + (1.0 / 16 if seeded else 0.0))
     share = rec["exact_group_tile_share"] if rec else None
-    f32 = bf16 * share if share is not None else 0.0
+    f32 = 2.0 * nu * I * D * share if share is not None else 0.0
     achieved = (bf16 + f32 * BF16_MFMA_PEAK_TF / F32_MFMA_PEAK_TF) / tk / 1e12
     return {"bound": "mfma", "achieved": achieved, "peak": BF16_MFMA_PEAK_TF,
             "unit": "TFLOP/s (bf16-equivalent MFMA work)", "frac": achieved / BF16_MFMA_PEAK_TF,

@@ -155,7 +155,10 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
  * lg_bound_prep_f32's bf16 copies of eu / ei (16-byte aligned); umarg[u] (fp32, per user)
  * must be >= 0.00785 ||eu[u]|| max_i ||ei[i]|| (lgcnhs.ops uses 0.0081 with the rounded-up
  * norms of lg_bound_prep_f32), the bound on |bf16 product - fp32 chain| of gbound.hip.
- * Workspace and splits as lg_score_topk_f32. */
+ * Workspace and splits as lg_score_topk_f32. For k <= 32 on catalogs of >= 1024 k items a
+ * screen-only seed pass over the first 1/16 of the items runs first and leaves each user's
+ * starting threshold in out_val[u * k + k - 1] (overwritten by the result); the outputs do
+ * not depend on it. */
 int lg_score_topk_screened_f32(const float *eu, const float *ei, const void *eu_bf16,
                                const void *ei_bf16, const float *umarg, int64_t n_users,
                                int64_t n_items, int32_t dim, const int64_t *ex_rowptr,

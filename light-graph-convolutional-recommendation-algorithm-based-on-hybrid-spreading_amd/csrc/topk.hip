@@ -321,16 +321,40 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
 // recomputed holds no score above any threshold, so k_score_topk would have inserted
 // nothing from it either: the lists (values, ids, order) are k_score_topk's exactly. While a
 // user's list can still take the mask value (thr = -inf) every tile is recomputed.
+//
+// Seeded entry thresholds (k <= 32). In a streaming top-K most insertions happen early:
+// k ln(N / k) of them over N items, three quarters within the first 1/16 of the range, and
+// while the thresholds are that low nearly every tile is recomputed exactly and inserted. So
+// a first, screen-only pass (SEEDP) over the first 1/16 of the items keeps, per user, the
+// largest LOWER bound fl(bf16 product - m_u) (nudged down: <= the item's exact score) of each
+// of C classes of items (item index mod C, C = 16 x the tiles per ring chunk, at most 64),
+// no insertions at all. If E_u of the user's excluded items lie in that range, the
+// (K + E_u)-th largest class maximum s_u is a lower bound of the final K-th value: K + E_u
+// distinct items reach it, at most E_u of them excluded (their final value is the mask value),
+// so K scoring items of the catalog score >= s_u (no seed when K + E_u > C). The main pass
+// starts every user's threshold at the float below s_u and never lets it fall under that, so
+// items that can not reach the final list are screened out from the first tile. The lists are
+// unchanged: every item of the final list scores >= its K-th value >= s_u and still enters.
+// Several splits: each split's seed is valid on its own, the largest is kept.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int D, int NG, int M, int WAVES, bool SH>
+// the largest float below a finite x
+__device__ __forceinline__ float next_below(float x) {
+  const int32_t b = __builtin_bit_cast(int32_t, x);
+  if (x == 0.f) return -__builtin_bit_cast(float, 1);  // (-0 as well)
+  return __builtin_bit_cast(float, x > 0.f ? b - 1 : b + 1);
+}
+
+template <int D, int NG, int M, int WAVES, bool SH, bool SEEDP>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
     const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
     int64_t n_items, const int64_t *__restrict__ ex_rowptr,
     const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
-    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx,
+    const float *__restrict__ seed_val) {
+  static_assert(!SEEDP || SH, "the seed pass is a mode of the shared-fragment kernel");
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
   // (SH: 48 entries per list -- k + 12 <= 32 held, + 16 per tile -- so the fragment ring gets
@@ -340,8 +364,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
 #endif
   constexpr int CAP = SH ? LG_RING_CAP : 64 * M;
   static_assert(!SH || M == 1, "the shared-fragment kernel is the k <= 32 one");
-  __shared__ float cs[WAVES][NG][16][CAP];
-  __shared__ int ci[WAVES][NG][16][CAP];
+  // seed classes: 16 x the tiles per ring chunk, at most 4 (one class per lane)
+  constexpr int TPC_S = 512 * WAVES / D / 16 < 4 ? 512 * WAVES / D / 16 : 4;
+  constexpr int NCLS = 16 * TPC_S;
+  // (the seed pass keeps its class maxima in cs instead of lists: no ids)
+  __shared__ float cs[WAVES][NG][16][SEEDP ? NCLS : CAP];
+  __shared__ int ci[WAVES][NG][16][SEEDP ? 1 : CAP];
   __shared__ int exs[WAVES][64];
 
   const int wave = threadIdx.x / 64;
@@ -367,12 +395,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   int64_t ex_pos[NG], ex_hi[NG];
   int cnt[NG], chk[NG];
   float tau[NG], thr[NG];
+  float sthr[NG];  // the seeded floor of thr (-inf without a seed)
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int64_t u = ubase + g * 16 + ul;
     uvalid[g] = u < n_users;
     const int64_t uu = uvalid[g] ? u : n_users - 1;
-    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+    sthr[g] = neg_inf<float>();
+    if (seed_val) {  // (a non-finite seed -- NaN embeddings -- seeds nothing)
+      const float sv = seed_val[uu * k + k - 1];
+      if (sv > neg_inf<float>() && sv < __builtin_huge_valf())
+        sthr[g] = next_below(sv);
+    }
+    if constexpr (!SEEDP) load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
 #pragma unroll
     for (int s = 0; s < S; ++s)
       ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
@@ -386,7 +421,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     cnt[g] = 0;
     chk[g] = 0;
     tau[g] = neg_inf<float>();
-    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
+    thr[g] = uvalid[g] ? sthr[g] : __builtin_huge_valf();
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
   // retire the prologue loads with a wait hipcc sees (vmcnt(0)): otherwise its waitcnt pass
@@ -437,7 +472,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       chk[g] = nc;
       tau[g] = t;
       ex_pos[g] = pos;
-      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
+      thr[g] = !uvalid[g] ? __builtin_huge_valf()
+                          : fmaxf(mask_value > t ? neg_inf<float>() : t, sthr[g]);
     }
   };
   auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
@@ -475,9 +511,34 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     it = it < n_items ? it : n_items - 1;
     load_piece<Q>(ei + it * D + gq * Q, af);
   };
-  auto exact_from = [&](int t, const bool (&gh)[NG], const float (&af)[Q])
+  // insertion of tile t's scores acc[g] (lane (ul, gq): item 4 gq + r of the tile, user ul)
+  // into the lists of the groups gh, against thr
+  auto insert_acc = [&](int t, const bool (&gh)[NG], const f32x4 (&accs)[NG])
       __attribute__((always_inline)) {
     const int rel = t * 16 + gq * 4;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (!gh[g]) continue;
+      const f32x4 acc = accs[g];
+      if (__ballot(above(max4(acc), thr[g])) == 0) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sc = acc[r];
+        const bool cand = rel + r < n_valid && sc > thr[g];
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+          if (cand) {
+            cs[wave][g][ul][pos] = sc;
+            ci[wave][g][ul][pos] = (int)i0 + rel + r;
+          }
+          cnt[g] += __popcll(bal & same_user);
+        }
+      }
+    }
+  };
+  auto exact_from = [&](int t, const bool (&gh)[NG], const float (&af)[Q])
+      __attribute__((always_inline)) {
     bool all = true;
 #pragma unroll
     for (int g = 0; g < NG; ++g) all &= gh[g];
@@ -500,26 +561,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
           accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
       }
     }
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (!gh[g]) continue;
-      const f32x4 acc = accs[g];
-      if (__ballot(above(max4(acc), thr[g])) == 0) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float sc = acc[r];
-        const bool cand = rel + r < n_valid && sc > thr[g];
-        const uint64_t bal = __ballot(cand);
-        if (bal) {
-          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
-          if (cand) {
-            cs[wave][g][ul][pos] = sc;
-            ci[wave][g][ul][pos] = (int)i0 + rel + r;
-          }
-          cnt[g] += __popcll(bal & same_user);
-        }
-      }
-    }
+    insert_acc(t, gh, accs);
   };
   auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
     float af[Q];
@@ -554,6 +596,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       maybe_compact(l < lim_end ? l : lim_end);
     }
   };
+  // the seed pass's class maxima (SEEDP only)
+  f32x4 cmax[NG][SEEDP ? TPC_S : 1];
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int tt = 0; tt < (SEEDP ? TPC_S : 1); ++tt)
+      cmax[g][tt] = f32x4{neg_inf<float>(), neg_inf<float>(), neg_inf<float>(),
+                          neg_inf<float>()};
   if constexpr (SH) {
     // The block's waves share the bf16 item fragments through LDS: chunks of CI items (8 KiB,
     // one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a ring of
@@ -661,6 +711,25 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
                                                                   accb[tt][g], 0, 0, 0);
         }
       signal(&done[c % NBUF]);  // (the fragments are in registers: the buffer is free)
+      if constexpr (SEEDP) {
+        // the seed pass: each lane's running maxima of the lower bounds fl(bf16 product - m_u)
+        // (nudged down past the subtraction's rounding; past the range: -inf; a NaN stays NaN
+        // and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
+#pragma unroll
+        for (int tt = 0; tt < TPC; ++tt) {
+          const int rel = (t0 + tt) * 16 + gq * 4;
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = accb[tt][g][r] - marg[g];
+              const float lb = rel + r < n_valid ? d - (fabsf(d) * 0x1p-22f + 1e-30f)
+                                                 : neg_inf<float>();
+              cmax[g][tt % TPC_S][r] = __builtin_elementwise_maximum(cmax[g][tt % TPC_S][r], lb);
+            }
+        }
+        continue;
+      }
       uint32_t hits = 0;  // bit tt * NG + g: group g's screen hit in tile tt (wave-uniform)
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt)
@@ -727,6 +796,49 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   }
 
   wave_sync();
+  if constexpr (SEEDP) {
+    // per user: the (k + E)-th largest of its NCLS class maxima (E = its excluded items in this
+    // split's range), into the K-th slot of its output row; -inf when k + E > NCLS
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int tt = 0; tt < TPC_S; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[wave][g][ul][16 * tt + 4 * gq + r] = cmax[g][tt][r];
+    wave_sync();
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      for (int u = 0; u < 16; ++u) {
+        const int64_t user = ubase + g * 16 + u;
+        if (user >= n_users) break;
+        int E = 0;
+        if (ex_rowptr) {
+          const int64_t e1 = ex_rowptr[user + 1];
+          for (int64_t e = ex_rowptr[user] + lane; __ballot(e < e1) != 0; e += 64) {
+            const int32_t x = e < e1 ? ex_col[e] : -1;
+            E += __popcll(__ballot(x >= i0 && x < i1));
+          }
+        }
+        const int need = k + E;  // (wave-uniform)
+        float sv = neg_inf<float>();
+        if (need <= NCLS) {
+          const float v = lane < NCLS ? cs[wave][g][u][lane] : neg_inf<float>();
+          int rank = 0;  // entries above v, ties by class index
+          for (int j = 0; j < NCLS; ++j) {
+            const float w = cs[wave][g][u][j];
+            rank += (w > v || (w == v && j < lane)) ? 1 : 0;
+          }
+          const uint64_t b = __ballot(lane < NCLS && rank == need - 1);
+          if (b) sv = __shfl(v, __ffsll((long long)b) - 1);
+        }
+        if (lane == 0) {
+          if (n_splits == 1) out_val[user * k + k - 1] = sv;
+          else part_val[((int64_t)split * n_users + user) * k + k - 1] = sv;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     for (int u = 0; u < 16; ++u) {
@@ -874,6 +986,15 @@ static int topk_probe() {
 #else
 static int topk_probe() { return 0; }
 #endif
+// seeded thresholds in the screened top-K (measurement builds may turn them off:
+// -DLG_TOPK_SEED=0)
+#ifndef LG_TOPK_SEED
+#define LG_TOPK_SEED 1
+#endif
+static bool lg_topk_seeding() { return LG_TOPK_SEED != 0; }
+#ifndef LG_TOPK_SEED_DIV  // the seed pass covers the first 1/LG_TOPK_SEED_DIV of the items
+#define LG_TOPK_SEED_DIV 16
+#endif
 
 template <int D, int NG, int M, int WAVES>
 static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
@@ -912,28 +1033,43 @@ static void dispatch_topk(int M, const float *eu, const float *ei, int64_t n_use
                             stream);
 }
 
+// the seed pass's per-split seeds (slot K - 1 of each partial row): the largest of them
+__global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ part_val,
+                                                      int64_t n_users, int k, int n_splits,
+                                                      float *__restrict__ out_val) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n_users) return;
+  float m = neg_inf<float>();
+  for (int p = 0; p < n_splits; ++p) {
+    const float v = part_val[((int64_t)p * n_users + u) * k + k - 1];
+    m = v > m ? v : m;  // (a NaN seeds nothing)
+  }
+  out_val[u * k + k - 1] = m;
+}
+
 template <int D>
-static void dispatch_topk_screen(int M, const float *eu, const float *ei, const __bf16 *eub,
-                                 const __bf16 *eib, const float *umarg, int64_t n_users,
-                                 int64_t n_items, const int64_t *ex_rowptr,
+static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float *ei,
+                                 const __bf16 *eub, const __bf16 *eib, const float *umarg,
+                                 int64_t n_users, int64_t n_items, const int64_t *ex_rowptr,
                                  const int32_t *ex_col, float mask_value, int k, int n_splits,
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
-                                 float *part_val, int32_t *part_idx, hipStream_t stream) {
-#define LG_SCREEN_LAUNCH(NG, MM, W, SH)                                                        \
+                                 float *part_val, int32_t *part_idx, const float *seed_val,
+                                 hipStream_t stream) {
+#define LG_SCREEN_LAUNCH(NG, MM, W, SH, SEEDP)                                                 \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_score_topk_screen<D, NG, MM, W, SH><<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, \
-                                        stream>>>(eu, ei, eub, eib, umarg, n_users, n_items,  \
-                                                  ex_rowptr, ex_col, mask_value, k, n_splits, \
-                                                  items_per_split, out_val, out_idx, part_val, \
-                                                  part_idx);                                  \
+    k_score_topk_screen<D, NG, MM, W, SH, SEEDP>                                              \
+        <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
+            eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
+            n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
   // k <= 32: one 8-wave block per CU (128 KiB of lists + the 24 KiB fragment ring) shares
   // the item fragments; larger lists keep 2-wave blocks that load their own
-  if (M == 1) LG_SCREEN_LAUNCH(2, 1, 8, true)
-  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2, false)
-  else LG_SCREEN_LAUNCH(1, 4, 2, false)
+  if (M == 1 && seedp) LG_SCREEN_LAUNCH(2, 1, 8, true, true)
+  else if (M == 1) LG_SCREEN_LAUNCH(2, 1, 8, true, false)
+  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2, false, false)
+  else LG_SCREEN_LAUNCH(1, 4, 2, false, false)
 #undef LG_SCREEN_LAUNCH
 }
 
@@ -1041,21 +1177,41 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
   hipStream_t s = (hipStream_t)stream;
   const int M = cap_m(k);
   const __bf16 *ub = (const __bf16 *)eu_bf16, *ib = (const __bf16 *)ei_bf16;
-  switch (dim) {
-    case 32: dispatch_topk_screen<32>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
-    case 64: dispatch_topk_screen<64>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
-    default: dispatch_topk_screen<128>(M, eu, ei, ub, ib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k, ns, per, out_val, out_idx, part_val, part_idx, s); break;
+  auto pass = [&](bool seedp, int64_t n_it, int nsp, int64_t per_sp, const float *seed) {
+    switch (dim) {
+      case 32: dispatch_topk_screen<32>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
+      case 64: dispatch_topk_screen<64>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
+      default: dispatch_topk_screen<128>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
+    }
+    int st = launch_status("lg_score_topk_screened_f32");
+    if (st != LG_OK || nsp == 1) return st;
+    if (seedp) {  // the splits' seeds: the largest, into the K-th slot of each output row
+      k_seed_combine<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0, s>>>(
+          part_val, n_users, k, nsp, out_val);
+      return launch_status("lg_score_topk_screened_f32(seeds)");
+    }
+    const unsigned blocks = (unsigned)((n_users + 3) / 4);
+    if (k <= 64)
+      k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, nsp,
+                                                          out_val, out_idx);
+    else
+      k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, nsp,
+                                                          out_val, out_idx);
+    return launch_status("lg_score_topk_screened_f32(merge)");
+  };
+  // the seed pass (k <= 32, large catalogs): the screen-only top-K of the lower bounds over
+  // the first 1/16 of the items, into out_val (the main pass reads each user's K-th value
+  // there before it writes anything: a user's seed and its list belong to the same wave), on
+  // as many splits as the main pass (its partial lists fit the same workspace)
+  const int64_t n_seed = n_items / LG_TOPK_SEED_DIV / 16 * 16;
+  const bool seeded = M == 1 && lg_topk_seeding() && n_seed >= (int64_t)k * 64;
+  if (seeded) {
+    const int64_t per_s = split_len(n_seed, ns);
+    const int ns_s = (int)((n_seed + per_s - 1) / per_s);
+    const int st = pass(true, n_seed, ns_s, per_s, nullptr);
+    if (st != LG_OK) return st;
   }
-  int st = launch_status("lg_score_topk_screened_f32");
-  if (st != LG_OK || ns == 1) return st;
-  const unsigned blocks = (unsigned)((n_users + 3) / 4);
-  if (k <= 64)
-    k_topk_merge<2><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
-                                                        out_val, out_idx);
-  else
-    k_topk_merge<4><<<dim3(blocks), dim3(256), 0, s>>>(part_val, part_idx, n_users, k, ns,
-                                                        out_val, out_idx);
-  return launch_status("lg_score_topk_screened_f32(merge)");
+  return pass(false, n_items, ns, per, seeded ? out_val : nullptr);
 }
 
 extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_users,

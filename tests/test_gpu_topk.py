@@ -112,6 +112,44 @@ def test_screened_topk_non_finite_rows():
     assert (i[np.arange(U) != 7] >= 0).all() and not (i == 1234).any()
 
 
+@pytest.mark.parametrize("k", [1, 20, 32])
+def test_seeded_topk_exclusions_in_seed_range(k):
+    """The screened kernel's seed pass (k <= 32, catalogs of >= 1024 k items): every user's
+    threshold starts at the (k + E)-th largest class maximum of the lower bounds over the first
+    1/16 of the items, E = its excluded items there. Users whose best items of that range are
+    excluded (E from 0 to 60: the seed must skip them, and there is none once k + E > 64), items
+    tied in bf16 and exactly inside the range, a zero user, users scaled over 1e-2..1e2: the
+    lists equal the plain kernel's and the C oracle's bit for bit."""
+    from lgcnhs import ops
+    U, I, d = 200, 65536, 64
+    eu, ei = _emb(U, d, 51 + k), _emb(I, d, 52)
+    ei[100:140] = ei[60:100]  # exact ties inside the seed range
+    g = torch.Generator().manual_seed(53)
+    eu *= torch.exp(torch.randn(U, 1, generator=g) * 1.5)
+    eu[9] = 0.0
+    n_seed = I // 16
+    G = O.chain_scores(eu.numpy(), ei[:n_seed].numpy())
+    us, its = [], []
+    for u in range(U):
+        e = (u * 7) % 61  # 0..60 of the user's best seed-range items excluded
+        top = np.argsort(-G[u], kind="stable")[:e]
+        us += [u] * e
+        its += top.tolist()
+    rng = np.random.default_rng(54)
+    extra = rng.integers(0, I, 2000)
+    us += rng.integers(0, U, 2000).tolist()
+    its += extra.tolist()
+    rp, col = O.exclusion_csr(U, I, (np.array(us), np.array(its)))
+    ex = _rowsets(rp, col, U, I)
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    for ns in (1, None):
+        v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, n_splits=ns, screen=True)
+        v0, i0 = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, n_splits=ns, screen=False)
+        assert torch.equal(i, i0) and torch.equal(v.view(torch.int32), v0.view(torch.int32))
+        np.testing.assert_array_equal(i.cpu().numpy(), oi)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
 def test_score_topk_edge_cases():
     from lgcnhs import ops
     # fewer items than k (padding), all-excluded user (mask values surface), ties (equal
