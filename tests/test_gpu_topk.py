@@ -94,12 +94,14 @@ def test_screened_topk_near_ties_and_wide_norms():
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
-def test_screened_topk_non_finite_rows():
+@pytest.mark.parametrize("I", [3000, 40000])
+def test_screened_topk_non_finite_rows(I):
     """A NaN item row makes every user's screen margin NaN and a NaN user row its own: the
     screen then recomputes every tile of those users exactly, so the lists stay the plain
-    kernel's bit for bit (NaN scores never enter), and finite items still fill them."""
+    kernel's bit for bit (NaN scores never enter), and finite items still fill them. At
+    40,000 items the seed pass runs too: NaN lower bounds seed nothing."""
     from lgcnhs import ops
-    U, I, d, k = 64, 3000, 64, 20
+    U, d, k = 64, 64, 20
     eu, ei = _emb(U, d, 41), _emb(I, d, 42)
     ei[1234] = float("nan")
     eu[7] = float("nan")
