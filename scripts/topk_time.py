@@ -20,7 +20,11 @@ ap.add_argument("--modes", default="screen,plain")
 ap.add_argument("--splits", default="auto,1")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--users", type=int, default=32768)
+ap.add_argument("--margin-scale", type=float, default=1.0,
+                help="measurement only: scale the screen margin (below 1 it is no longer a "
+                     "proven bound; lists may differ)")
 args = ap.parse_args()
+ops.SCREEN_MARGIN *= args.margin_scale
 
 dev = torch.device("cuda:0")
 U, I, k = args.users, 1_000_000, 20
