@@ -364,7 +364,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
 #endif
   constexpr int CAP = SH ? LG_RING_CAP : 64 * M;
   static_assert(!SH || M == 1, "the shared-fragment kernel is the k <= 32 one");
-  // seed classes: 16 x the tiles per ring chunk, at most 4 (one class per lane)
+  // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane)
   constexpr int TPC_S = 512 * WAVES / D / 16 < 4 ? 512 * WAVES / D / 16 : 4;
   constexpr int NCLS = 16 * TPC_S;
   // (the seed pass keeps its class maxima in cs instead of lists: no ids)
@@ -1199,10 +1199,11 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
                                                           out_val, out_idx);
     return launch_status("lg_score_topk_screened_f32(merge)");
   };
-  // the seed pass (k <= 32, large catalogs): the screen-only top-K of the lower bounds over
-  // the first 1/16 of the items, into out_val (the main pass reads each user's K-th value
-  // there before it writes anything: a user's seed and its list belong to the same wave), on
-  // as many splits as the main pass (its partial lists fit the same workspace)
+  // the seed pass (k <= 32, large catalogs): the screen-only lower-bound class maxima over the
+  // first 1/16 of the items, each user's seed into the K-th slot of its out_val row (the main
+  // pass reads it there before it writes anything: a user's seed and its list belong to the
+  // same wave), on at most as many splits as the main pass (their seeds fit the same
+  // workspace; the largest is kept)
   const int64_t n_seed = n_items / LG_TOPK_SEED_DIV / 16 * 16;
   const bool seeded = M == 1 && lg_topk_seeding() && n_seed >= (int64_t)k * 64;
   if (seeded) {
