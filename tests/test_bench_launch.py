@@ -53,3 +53,25 @@ def test_world_size_must_match_gpus():
     p = _run(["--gpus", "2", "--launch-check"], _env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"))
     assert p.returncode != 0
     assert "WORLD_SIZE=3" in p.stderr
+
+
+def test_topk_roofline_prices_the_seed_pass_and_the_recorded_exact_share():
+    """bench.topk_roofline: bf16 work = the screen of every (user, item) plus, for k <= 32 on a
+    large catalog, the seed pass's screen of the first 1/16 of the items; the fp32 exact work
+    comes from the PMC record of this topk.hip (profiles/pmc_topk.json), priced at the bf16 /
+    fp32 MFMA peak ratio."""
+    sys.path.insert(0, REPO)
+    import bench
+    nu, I, D, t = 32768, 1_000_000, 64, 0.0125
+    r = bench.topk_roofline(nu, I, D, 20, t)
+    share = r["exact_group_tile_share"]
+    assert r["record_source"]["status"] == "measured" and 0.0 < share < 0.2
+    base = 2.0 * nu * I * D
+    want = (base * (1 + 1 / 16) + base * share * bench.BF16_MFMA_PEAK_TF /
+            bench.F32_MFMA_PEAK_TF) / t / 1e12
+    assert abs(r["achieved"] - want) < 1e-9 * want
+    assert abs(r["frac"] - want / bench.BF16_MFMA_PEAK_TF) < 1e-12
+    # k > 32: no seed pass; a shape without a record: the screen alone, flagged
+    r2 = bench.topk_roofline(nu, I, D, 33, t)
+    assert r2["exact_group_tile_share"] is None
+    assert abs(r2["achieved"] - base / t / 1e12) < 1e-9 * r2["achieved"]
