@@ -221,41 +221,72 @@ def cpu_baseline_spread(k, lam=0.5):
                       f"{du} users x {di} items, {de} Zipf interactions (c3_douban_shape)"}
 
 
-def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev):
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
+
+
+def time_propagation(shard, dis_l, e0_orig, D, L, steps, warmup, world, dev, layer_fn=None):
     """Time `steps` full L-layer forwards; returns (max-over-ranks seconds, average SpMM
-    'launch' seconds = one layer's kernels on this rank, from HIP events on the stream)."""
-    from lgcnhs.dist import BipartitePropagation, SegmentShard, ShardedPropagation
+    'launch' seconds = one layer's kernels on this rank, from HIP events on the stream, and
+    at N > 1 the `comm` block). layer_fn: lgcnhs.dist's HIP layer unless given (the CPU
+    launch check passes a host stand-in)."""
+    from lgcnhs.dist import BipartitePropagation, SegmentShard, ShardedPropagation, exposed_wait_ms
     e0 = shard.permute_rows(e0_orig)  # chunk-major layout (identity at N=1)
     cls = BipartitePropagation if isinstance(shard, SegmentShard) else ShardedPropagation
-    prop = cls(shard, dis_l, D, L, dev)
+    kw = {} if layer_fn is None else {"layer_fn": layer_fn}
+    prop = cls(shard, dis_l, D, L, dev, **kw)
     for _ in range(warmup):
         prop.forward(e0)
-    torch.cuda.synchronize()
-    prop.events = []
+    _sync(dev)
+    cuda = torch.device(dev).type == "cuda"
+    prop.events = [] if cuda else None
+    prop.waits = []
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t1 = time.perf_counter()
     for _ in range(steps):
         prop.forward(e0)
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t1
-    kernel_ms = sum(s.elapsed_time(e) for s, e in prop.events)  # SpMM kernels only
+    kernel_ms = sum(s.elapsed_time(e) for s, e in prop.events) if cuda else 0.0  # SpMM only
     comm = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        wait = exposed_wait_ms(prop.waits, L, steps)
+        prop.waits = None
         comm = time_exchange(prop, shard, D, world, dev)
+        comm.update(exposure(wait, comm["allgather_ms_per_layer"], L, world, dev))
     del prop, e0
     return elapsed, kernel_ms / (steps * L) / 1e3, comm
 
 
+def exposure(wait_ms, ag_ms, L, world, dev):
+    """The part of the exchange the overlapped forward did not hide: per layer, the compute
+    stream's stall on the gathers it awaited (lgcnhs.dist._WaitTimer; the stall of layer l is
+    the wait for layer l-1's gathers), max over ranks; against the L - 1 layers' gathers timed
+    alone (`allgather_ms_per_layer`): hidden_frac = 1 - exposed / isolated."""
+    t = torch.tensor(wait_ms, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = [float(v) for v in t.tolist()]
+    iso = (L - 1) * ag_ms
+    tot = sum(per)
+    return {"exposed_wait_ms_per_layer": per, "exposed_wait_ms": tot,
+            "isolated_allgather_ms_per_step": iso,
+            "hidden_frac": (1.0 - tot / iso) if iso > 0 else None}
+
+
 def time_exchange(prop, shard, D, world, dev, reps=5):
-    """The all-gathers of one layer alone (no SpMM running): RCCL over xGMI, ms per layer
-    and GB/s received per GPU ((W-1)/W of the padded [n, D] fp32 table)."""
+    """The all-gathers of one layer alone (no SpMM running): RCCL over xGMI, ms per layer.
+    Rates as nccl-tests defines them for all_gather of a total output of S bytes (the padded
+    [n, D] fp32 table): algbw = S / t, busbw = algbw (W - 1) / W -- what each GPU receives
+    per second, the figure to hold against xGMI's per-link rate."""
     from lgcnhs.dist import SegmentShard, _gather_block, _gather_piece
     buf = prop.bufs[0]
 
@@ -271,18 +302,20 @@ def time_exchange(prop, shard, D, world, dev, reps=5):
         for h in hs:
             h.wait()
     once()
-    torch.cuda.synchronize()
+    _sync(dev)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         once()
-    torch.cuda.synchronize()
+    _sync(dev)
     dt = (time.perf_counter() - t0) / reps
     t = torch.tensor([dt], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    recv = (world - 1) / world * shard.n_pad * D * 4
-    return {"allgather_ms_per_layer": dt * 1e3, "recv_GBps_per_gpu": recv / dt / 1e9,
+    size = shard.n_pad * D * 4
+    recv = (world - 1) / world * size
+    return {"allgather_ms_per_layer": dt * 1e3, "algbw_GBps": size / dt / 1e9,
+            "busbw_GBps": recv / dt / 1e9, "recv_GBps_per_gpu": recv / dt / 1e9,
             "recv_bytes_per_gpu": recv, "pad_ratio": shard.pad_ratio}
 
 
@@ -739,30 +772,70 @@ def wants_cpu_baseline(rank: int, args) -> bool:
     return rank == 0 and not args.no_cpu_baseline
 
 
+def _host_layer(shard, piece, dis, x, y, x0, acc, out, mode, denom):
+    """Host (torch CPU) stand-in for lgcnhs.dist.hip_layer over one piece of a shard, for
+    the CPU launch check only: the same modes as lg_spmm_layer_f32 (1 FIRST, 2 MID, 3 LAST,
+    4 FIRST+LAST)."""
+    lb, le, off = piece
+    if le <= lb:
+        return
+    rp = shard.rowptr
+    e0, e1 = int(rp[lb]), int(rp[le])
+    srcs = shard.src[e0:e1].long()
+    rows = torch.repeat_interleave(torch.arange(le - lb), (rp[lb + 1:le + 1] - rp[lb:le]))
+    w = dis[srcs] * dis[rows + off]
+    v = torch.zeros(le - lb, x.shape[1]).index_add_(0, rows, w[:, None] * x[srcs])
+    g = slice(off, off + le - lb)
+    if y is not None:
+        y[g] = v
+    if mode == 1:
+        acc[g] = x0[g] + v
+    elif mode == 2:
+        acc[g] += v
+    elif mode == 3:
+        out[g] = (acc[g] + v) / denom
+    elif mode == 4:
+        out[g] = (x0[g] + v) / denom
+
+
 def launch_check(world: int, rank: int, args) -> None:
     """--launch-check: the rank plumbing alone (process group, one all-reduce, rank 0's
     JSON line), no GPU work; what the CPU tests drive through launch_ranks(). Rank 0 also
     runs the propagation CPU baseline on a small CPU graph through the same function and
-    rank rule as the real line, so the N > 1 cpu_baseline field is exercised without a GPU."""
+    rank rule as the real line, and at N > 1 every rank times the overlapped bipartite
+    forward over gloo through time_propagation, so the N > 1 cpu_baseline and comm fields are
+    exercised without a GPU."""
     t = torch.ones(1)
     if world > 1:
         dist.all_reduce(t)
+    g = torch.Generator().manual_seed(0)  # a small symmetric bipartite CSR, built on CPU
+    U, I = 300, 400
+    keys = torch.unique(torch.randint(0, U, (5000,), generator=g) * I +
+                        torch.randint(0, I, (5000,), generator=g))
+    rows = torch.cat([keys // I, keys % I + U])
+    cols = torch.cat([keys % I + U, keys // I])
+    order = torch.argsort(rows * (U + I) + cols)
+    rows, src = rows[order], cols[order].to(torch.int32)
+    rp = torch.zeros(U + I + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(torch.bincount(rows, minlength=U + I), 0)
+    comm = None
+    if world > 1:
+        # the N > 1 line's comm block through the real timing code: the bipartite shards and
+        # the overlapped forward over gloo, a host stand-in for the HIP layer
+        from lgcnhs.dist import SegmentShard
+        shard = SegmentShard(rp, src, [0, U, U + I], rank, world, "cpu", chunks=2)
+        deg = (rp[1:] - rp[:-1]).float()
+        dis = torch.where(deg > 0, deg.pow(-0.5), torch.zeros_like(deg))
+        e0 = torch.randn(U + I, 16, generator=g) * 0.1
+        _, _, comm = time_propagation(shard, shard.permute_rows(dis), e0, 16, 3, 2, 1, world,
+                                      "cpu", layer_fn=_host_layer)
     cpu = None
     if wants_cpu_baseline(rank, args):
-        g = torch.Generator().manual_seed(0)  # a small symmetric bipartite CSR, built on CPU
-        U, I = 300, 400
-        keys = torch.unique(torch.randint(0, U, (5000,), generator=g) * I +
-                            torch.randint(0, I, (5000,), generator=g))
-        rows = torch.cat([keys // I, keys % I + U])
-        cols = torch.cat([keys % I + U, keys // I])
-        order = torch.argsort(rows * (U + I) + cols)
-        rows, src = rows[order], cols[order].to(torch.int32)
-        rp = torch.zeros(U + I + 1, dtype=torch.int64)
-        rp[1:] = torch.cumsum(torch.bincount(rows, minlength=U + I), 0)
         cpu = cpu_baseline(rp, src, U + I, 16, 3, target_nnz=4000, reps=1)
     if rank == 0:
         print(json.dumps({"metric": "launch-check", "n_gpus": world,
-                          "ranks_seen": int(t.item()), "cpu_baseline": cpu}), flush=True)
+                          "ranks_seen": int(t.item()), "cpu_baseline": cpu, "comm": comm}),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

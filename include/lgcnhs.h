@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 11
+#define LG_ABI_VERSION 12
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -149,12 +149,16 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
                       float mask_value, int32_t k, int32_t n_splits, float *out_val,
                       int64_t *out_idx, void *ws, size_t ws_bytes, lg_stream_t stream);
 
-/* lg_score_topk_f32 with a bf16 MFMA screen (csrc/topk.hip K2s): the same outputs bit for
- * bit (values, ids, order), computing the exact fp32 chain only for 16-item tiles in which
- * some user's bf16 product plus umarg[u] can beat its entry threshold. eu_bf16 / ei_bf16:
- * lg_bound_prep_f32's bf16 copies of eu / ei (16-byte aligned); umarg[u] (fp32, per user)
- * must be >= 0.00785 ||eu[u]|| max_i ||ei[i]|| (lgcnhs.ops uses 0.0081 with the rounded-up
- * norms of lg_bound_prep_f32), the bound on |bf16 product - fp32 chain| of gbound.hip.
+/* lg_score_topk_f32 with a bf16 MFMA screen (csrc/topk.hip K2s/K2r): the same outputs bit
+ * for bit (values, ids, order). eu_bf16 / ei_bf16: lg_bound_prep_f32's bf16 copies of eu / ei
+ * (16-byte aligned). umarg[u] (fp32, per user) must bound |bf16 MFMA product - fp32 chain|
+ * over every item, with slack for the fp32 roundings of the screen's own compares:
+ *   umarg[u] >= (||du|| I + (||eu[u]|| + ||du||) DI + (2.01 dim 2^-24 + 2^-22) ||eu[u]|| I)
+ * with du = eu[u] - bf16(eu[u]), I = max_i ||ei[i]||, DI = max_i ||ei[i] - bf16(ei[i])||
+ * (lgcnhs.ops.screen_margins, from lg_bound_prep_f32's norm_up / err_up; the round-3 form
+ * 0.0081 ||eu[u]|| I is larger and also valid). k <= 32: one pass keeps per user the items
+ * whose bound can still reach the k-th largest lower bound, and ranks those by the exact chain
+ * at the end; k > 32: a tile whose bound beats a user's threshold is recomputed exactly.
  * Workspace and splits as lg_score_topk_f32. For k <= 32 on catalogs of >= 1024 k items a
  * screen-only seed pass over the first 1/16 of the items runs first and leaves each user's
  * starting threshold in out_val[u * k + k - 1] (overwritten by the result); the outputs do
@@ -348,9 +352,14 @@ int lg_spread_tile_resource_topk_f64(const int64_t *user_rowptr, const int32_t *
                                      int64_t n_ex_positions, lg_stream_t stream);
 
 /* x_bf16[r] = bf16(x[r]) (round to nearest even), norm_up[r] = ||x[r]||_2 rounded up to
- * fp32: the operands of lg_score_chunk_bound (csrc/gbound.hip). */
+ * fp32: the operands of lg_score_chunk_bound (csrc/gbound.hip). err_up (optional, may be
+ * NULL): err_up[r] = ||x[r] - x_bf16[r]||_2 rounded up, the rounding-error norms the
+ * screened top-K's margin umarg is built from (lgcnhs.ops.screen_margins). */
 int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
-                      float *norm_up, lg_stream_t stream);
+                      float *norm_up, float *err_up, lg_stream_t stream);
+
+/* Widest item tile lg_score_chunk_bound accepts (64 chunks of 64 columns). */
+#define LG_BOUND_MAX_WIDTH 4096
 
 /* gb[u][c] (fp32, [n_users][ceil(width / 64)]) >= the fp32 score chain e0_u . e0_j of every
  * column j of chunk c = [item_begin + 64c, item_begin + 64c + 64) of the tile: the bf16 MFMA
@@ -358,7 +367,7 @@ int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
  * lg_bound_prep_f32 of the users' rows and of all items. dim in {32, 64, 128}. qb (optional,
  * [n_users][qstride] bytes, qstride >= width rounded up to 256): per column j,
  * q = ceil(255 (G_bf16 + margin) / gb) in [0, 255], so gb * q / 255 >= the chain score too
- * (csrc/gbound.hip). */
+ * (csrc/gbound.hip). width <= LG_BOUND_MAX_WIDTH (LG_ERR_ARG otherwise). */
 int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int64_t n_users,
                          const void *i_bf16, const float *i_norm, int32_t dim,
                          int32_t item_begin, int32_t width, float *gb, uint8_t *qb,

@@ -31,6 +31,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBoundMargin = 0.008f;
+// widest tile lg_score_chunk_bound takes: 64 chunks of 64 columns (LG_BOUND_MAX_WIDTH)
+constexpr int kBoundMaxWidth = LG_BOUND_MAX_WIDTH;
 
 // max of three floats: one v_maximum3_f32 (gfx950), compiler-visible, so hipcc pads the
 // MFMA-result wait states itself (no NaN-quieting canonicalisation as fmaxf would add; the
@@ -60,25 +62,37 @@ __device__ __forceinline__ float round_up_f32(double x) {
   return f;
 }
 
-// xb[r] = bf16(x[r]) (round to nearest even), norm[r] = ||x[r]||_2 rounded up to fp32.
-// One wave per row.
+// xb[r] = bf16(x[r]) (round to nearest even), norm[r] = ||x[r]||_2 rounded up to fp32, and
+// (err, optional) err[r] = ||x[r] - bf16(x[r])||_2 rounded up: the per-row rounding error the
+// screened top-K's tight margin is built from (lgcnhs.ops.screen_margins). x - bf16(x) is
+// exact in fp32 (it has at most 16 significant bits). One wave per row.
 __global__ __launch_bounds__(256) void k_bound_prep(const float *__restrict__ x, int64_t n,
                                                     int dim, __bf16 *__restrict__ xb,
-                                                    float *__restrict__ norm) {
+                                                    float *__restrict__ norm,
+                                                    float *__restrict__ err) {
   const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
   if (r >= n) return;
   const int lane = lane_id();
-  double ss = 0.0;
+  double ss = 0.0, se = 0.0;
   for (int d = lane; d < dim; d += 64) {
     const float v = x[r * dim + d];
-    xb[r * dim + d] = (__bf16)v;
+    const __bf16 b = (__bf16)v;
+    xb[r * dim + d] = b;
     ss += (double)v * (double)v;
+    const double e = (double)v - (double)(float)b;
+    se += e * e;
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  for (int o = 32; o > 0; o >>= 1) {
+    ss += __shfl_xor(ss, o);
+    se += __shfl_xor(se, o);
+  }
   // sqrt of an fp64 sum of squares of fp32 values: relative error ~1e-16, far below the
   // fp32 round-up (the margin constant leaves 2 % slack besides)
-  if (lane == 0) norm[r] = round_up_f32(sqrt(ss) * (1.0 + 1e-12));
+  if (lane == 0) {
+    norm[r] = round_up_f32(sqrt(ss) * (1.0 + 1e-12));
+    if (err) err[r] = round_up_f32(sqrt(se) * (1.0 + 1e-12));
+  }
 }
 
 // One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile; a block = 4
@@ -152,9 +166,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       nrow_w > 0 ? (int)(nrow_w * nch * 4) : 0, 0x00020000);
   // every chunk's largest item norm (the margin's ||j|| factor), once per block: wave w folds
   // chunks w, w + 4, ... (the loads first, then the reductions side by side)
-  __shared__ float s_cmax[64];
+  __shared__ float s_cmax[kBoundMaxWidth / 64];
   {
-    constexpr int CPW = 16;  // chunks per wave (nch <= 64)
+    constexpr int CPW = kBoundMaxWidth / 64 / 4;  // chunks per wave (nch <= 64, checked at the ABI)
     float v[CPW];
 #pragma unroll
     for (int k = 0; k < CPW; ++k) {
@@ -308,12 +322,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 using namespace lg;
 
 extern "C" int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, void *x_bf16,
-                                 float *norm_up, lg_stream_t stream) {
+                                 float *norm_up, float *err_up, lg_stream_t stream) {
   LG_REQUIRE(x && x_bf16 && norm_up && n_rows >= 0 && dim >= 1,
              "lg_bound_prep_f32: bad arguments");
   if (n_rows == 0) return LG_OK;
   k_bound_prep<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
-      x, n_rows, dim, (__bf16 *)x_bf16, norm_up);
+      x, n_rows, dim, (__bf16 *)x_bf16, norm_up, err_up);
   return launch_status("lg_bound_prep_f32");
 }
 
@@ -328,6 +342,9 @@ extern "C" int lg_score_chunk_bound(const void *u_bf16, const float *u_norm, int
              "lg_score_chunk_bound: qstride %d < width %d rounded up to 256", qstride, width);
   LG_REQUIRE(dim == 32 || dim == 64 || dim == 128, "lg_score_chunk_bound: dim %d not in "
              "{32,64,128}", dim);
+  // the per-chunk norm maxima live in a 64-entry LDS table (s_cmax, 16 chunks per wave)
+  LG_REQUIRE(width <= kBoundMaxWidth, "lg_score_chunk_bound: width %d > %d", width,
+             kBoundMaxWidth);
   if (n_users == 0) return LG_OK;
   const int nch = (width + 63) / 64;
   const dim3 grid((unsigned)((n_users + 255) / 256));

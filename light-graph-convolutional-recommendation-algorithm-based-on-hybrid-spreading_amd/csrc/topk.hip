@@ -314,28 +314,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
 }
 // K2s: the same top-K with a bf16 MFMA screen (v_mfma_f32_16x16x32_bf16, 16x the f32
 // MFMA's rate). Per 16-item tile every user's bf16 product plus a rigorous margin m_u
-// (|G_bf16 - G_chain| <= 0.00785 ||u|| ||i||, csrc/gbound.hip; m_u = 0.0081 ||u|| max ||i||
-// >= it) is an upper bound of the exact fp32 chain score. Only a tile where some user's bound
-// beats its entry threshold is recomputed with the f32 MFMA chain of k_score_topk -- the
-// exact scores, bit for bit -- and runs k_score_topk's insertion on them. A tile that is not
-// recomputed holds no score above any threshold, so k_score_topk would have inserted
-// nothing from it either: the lists (values, ids, order) are k_score_topk's exactly. While a
-// user's list can still take the mask value (thr = -inf) every tile is recomputed.
-//
-// Seeded entry thresholds (k <= 32). In a streaming top-K most insertions happen early:
-// k ln(N / k) of them over N items, three quarters within the first 1/16 of the range, and
-// while the thresholds are that low nearly every tile is recomputed exactly and inserted. So
-// a first, screen-only pass (SEEDP) over the first 1/16 of the items keeps, per user, the
-// largest LOWER bound fl(bf16 product - m_u) (nudged down: <= the item's exact score) of each
-// of C classes of items (item index mod C, C = 16 x the tiles per ring chunk, at most 64),
-// no insertions at all. If E_u of the user's excluded items lie in that range, the
-// (K + E_u)-th largest class maximum s_u is a lower bound of the final K-th value: K + E_u
-// distinct items reach it, at most E_u of them excluded (their final value is the mask value),
-// so K scoring items of the catalog score >= s_u (no seed when K + E_u > C). The main pass
-// starts every user's threshold at the float below s_u and never lets it fall under that, so
-// items that can not reach the final list are screened out from the first tile. The lists are
-// unchanged: every item of the final list scores >= its K-th value >= s_u and still enters.
-// Several splits: each split's seed is valid on its own, the largest is kept.
+// (umarg, include/lgcnhs.h: |G_bf16 - G_chain| <= m_u for every item) is an upper bound of the
+// exact fp32 chain score. Only a tile where some user's bound beats its entry threshold is
+// recomputed with the f32 MFMA chain of k_score_topk -- the exact scores, bit for bit -- and
+// runs k_score_topk's insertion on them. A tile that is not recomputed holds no score above
+// any threshold, so k_score_topk would have inserted nothing from it either: the lists
+// (values, ids, order) are k_score_topk's exactly. While a user's list can still take the
+// mask value (thr = -inf) every tile is recomputed. This per-wave kernel serves k > 32; the
+// k <= 32 lists run k_topk_ring below.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // the largest float below a finite x
@@ -345,31 +331,19 @@ __device__ __forceinline__ float next_below(float x) {
   return __builtin_bit_cast(float, x > 0.f ? b - 1 : b + 1);
 }
 
-template <int D, int NG, int M, int WAVES, bool SH, bool SEEDP>
+template <int D, int NG, int M, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
     const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
     int64_t n_items, const int64_t *__restrict__ ex_rowptr,
     const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
-    float *__restrict__ part_val, int32_t *__restrict__ part_idx,
-    const float *__restrict__ seed_val) {
-  static_assert(!SEEDP || SH, "the seed pass is a mode of the shared-fragment kernel");
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
-  // (SH: 48 entries per list -- k + 12 <= 32 held, + 16 per tile -- so the fragment ring gets
-  // the LDS for 7 chunks)
-#ifndef LG_RING_CAP
-#define LG_RING_CAP 48
-#endif
-  constexpr int CAP = SH ? LG_RING_CAP : 64 * M;
-  static_assert(!SH || M == 1, "the shared-fragment kernel is the k <= 32 one");
-  // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane)
-  constexpr int TPC_S = 512 * WAVES / D / 16 < 4 ? 512 * WAVES / D / 16 : 4;
-  constexpr int NCLS = 16 * TPC_S;
-  // (the seed pass keeps its class maxima in cs instead of lists: no ids)
-  __shared__ float cs[WAVES][NG][16][SEEDP ? NCLS : CAP];
-  __shared__ int ci[WAVES][NG][16][SEEDP ? 1 : CAP];
+  constexpr int CAP = 64 * M;
+  __shared__ float cs[WAVES][NG][16][CAP];
+  __shared__ int ci[WAVES][NG][16][CAP];
   __shared__ int exs[WAVES][64];
 
   const int wave = threadIdx.x / 64;
@@ -379,9 +353,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   const int64_t tile = blockIdx.x / n_splits;
   const int split = blockIdx.x % n_splits;
   const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
-  // (SH: waves past the last user still stage their share of every chunk and meet every
-  // barrier; their users are invalid, so they never hit the screen and write nothing)
-  if (!SH && ubase >= n_users) return;  // wave-uniform; no block-level barriers below
+  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
   const int64_t i0 = (int64_t)split * items_per_split;
   int64_t i1 = i0 + items_per_split;
   if (i1 > n_items) i1 = n_items;
@@ -395,19 +367,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
   int64_t ex_pos[NG], ex_hi[NG];
   int cnt[NG], chk[NG];
   float tau[NG], thr[NG];
-  float sthr[NG];  // the seeded floor of thr (-inf without a seed)
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int64_t u = ubase + g * 16 + ul;
     uvalid[g] = u < n_users;
     const int64_t uu = uvalid[g] ? u : n_users - 1;
-    sthr[g] = neg_inf<float>();
-    if (seed_val) {  // (a non-finite seed -- NaN embeddings -- seeds nothing)
-      const float sv = seed_val[uu * k + k - 1];
-      if (sv > neg_inf<float>() && sv < __builtin_huge_valf())
-        sthr[g] = next_below(sv);
-    }
-    if constexpr (!SEEDP) load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
+    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
 #pragma unroll
     for (int s = 0; s < S; ++s)
       ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
@@ -421,13 +386,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     cnt[g] = 0;
     chk[g] = 0;
     tau[g] = neg_inf<float>();
-    thr[g] = uvalid[g] ? sthr[g] : __builtin_huge_valf();
+    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
   }
   const uint64_t same_user = 0x0001000100010001ull << ul;
   // retire the prologue loads with a wait hipcc sees (vmcnt(0)): otherwise its waitcnt pass
-  // merges their pending state into the loop header, and the screen loop's waits for them
-  // (vmcnt(0) on the user fragments and margins) also drained the fragment ring's DMA issued
-  // at the chunk start -- every chunk then waited for its successor's copy
+  // merges their pending state into the loop header and waits for them inside the loop
   __builtin_amdgcn_s_waitcnt(0x0F70);
   // compact (and raise the threshold) once k + 12 candidates are held: the screen's hit
   // rate follows the threshold
@@ -472,8 +435,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       chk[g] = nc;
       tau[g] = t;
       ex_pos[g] = pos;
-      thr[g] = !uvalid[g] ? __builtin_huge_valf()
-                          : fmaxf(mask_value > t ? neg_inf<float>() : t, sthr[g]);
+      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
     }
   };
   auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
@@ -502,17 +464,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     for (int s = 0; s < S; ++s)
       fr[s] = *reinterpret_cast<const bf16x8 *>(eib + it * D + 32 * s + 8 * gq);
   };
-  // the exact tile: k_score_topk's f32 chain, then its insertion against thr
-  // (only the user groups whose screen hit: a group's chain is its own 16-user MFMA column
-  // block, so the others' exact scores are not needed)
-  // fp32 fragments of tile t (clamped past the table)
-  auto load_exact = [&](int t, float (&af)[Q]) __attribute__((always_inline)) {
-    int64_t it = i0 + 16 * t + ul;
-    it = it < n_items ? it : n_items - 1;
-    load_piece<Q>(ei + it * D + gq * Q, af);
-  };
-  // insertion of tile t's scores acc[g] (lane (ul, gq): item 4 gq + r of the tile, user ul)
-  // into the lists of the groups gh, against thr
+  // insertion of tile t's exact scores acc[g] (lane (ul, gq): item 4 gq + r of the tile,
+  // user ul) into the lists of the groups gh, against thr
   auto insert_acc = [&](int t, const bool (&gh)[NG], const f32x4 (&accs)[NG])
       __attribute__((always_inline)) {
     const int rel = t * 16 + gq * 4;
@@ -537,65 +490,425 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       }
     }
   };
-  auto exact_from = [&](int t, const bool (&gh)[NG], const float (&af)[Q])
-      __attribute__((always_inline)) {
-    bool all = true;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) all &= gh[g];
+  // the exact tile: k_score_topk's f32 chain (only the user groups whose screen hit: a
+  // group's chain is its own 16-user MFMA column block), then its insertion against thr
+  auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
+    float af[Q];
+    int64_t it = i0 + 16 * t + ul;
+    it = it < n_items ? it : n_items - 1;
+    load_piece<Q>(ei + it * D + gq * Q, af);
     f32x4 accs[NG];
-    if (all) {  // every group: the chains interleave on the MFMA pipe
 #pragma unroll
-      for (int g = 0; g < NG; ++g) accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NG; ++g) {
+      accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!gh[g]) continue;  // (wave-uniform)
 #pragma unroll
       for (int s = 0; s < Q; ++s)
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!gh[g]) continue;  // (wave-uniform)
-#pragma unroll
-        for (int s = 0; s < Q; ++s)
-          accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
-      }
+        accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
     }
     insert_acc(t, gh, accs);
   };
-  auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
-    float af[Q];
-    load_exact(t, af);
-    exact_from(t, gh, af);
+
+  const int lim_end = (int)i1;
+  // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
+  // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
+  // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at
+  // C5, d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
+  bf16x8 fr[2][S];
+  load_bf(0, fr[0]);
+  load_bf(1, fr[1]);
+  for (int t0 = 0; t0 < n_t; t0 += 2) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int t = t0 + p;
+      if (t >= n_t) break;
+      f32x4 accb[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[p][s], ub[g][s], accb[g], 0, 0, 0);
+      }
+      load_bf(t + 2, fr[p]);  // tile t + 2 into the buffer tile t just left
+      bool gh[NG];
+      bool hit = false;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
+        gh[g] = __ballot(above(max4(accb[g]) + marg[g], thr[g])) != 0;
+        hit |= gh[g];
+      }
+      if (hit) {
+        exact_tile(t, gh);
+        const int l = (int)i0 + (t + 1) * 16;
+        maybe_compact(l < lim_end ? l : lim_end);
+      }
+    }
+  }
+
+  wave_sync();
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    for (int u = 0; u < 16; ++u) {
+      const int64_t user = ubase + g * 16 + u;
+      if (user >= n_users) break;
+      compact_user(g, u, lim_end);
+      const int nc = __shfl(cnt[g], u);
+      for (int e = lane; e < k; e += 64) {
+        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
+        const int id = e < nc ? ci[wave][g][u][e] : -1;
+        if (n_splits == 1) {
+          out_val[user * k + e] = v;
+          out_idx[user * k + e] = id;
+        } else {
+          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          part_val[o] = v;
+          part_idx[o] = id;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// K2r: the screened top-K for k <= 32, with bound-side lists -- no exact score inside the
+// streaming loop.
+//
+// Every item i of user u has, from its bf16 product b = G_bf16(u, i), a lower bound
+// LB = fl(b - m_u) and an upper bound UB = fl(b + m_u) of its exact chain score (nudged
+// outward past the roundings; excluded items and already exact entries have LB = UB = their
+// final value). A user's list holds (b, item) entries; at each compaction
+// tau = the k-th largest LB of the list. Every list entry whose UB is below tau (or below the
+// seed floor, below) can not be in the final top-k -- k items of lower id reach tau, which
+// exceeds its exact score -- and is dropped; an item enters only if fl(b + m_u) > tau, for the
+// same reason. Nothing else is dropped, so the final list holds every item of the exact
+// top-k; at the end of the stream its entries get the exact fp32 chain (k_score_topk's MFMA
+// chain, bit for bit), and the best k by (value desc, item asc) are the output -- identical to
+// k_score_topk's. If a compaction leaves more entries than a tile could still add room for,
+// the entries are made exact right there (the same chain) and the list cut to k.
+// The loop thus issues no load but the fragment ring's DMA, and a hit costs an insertion
+// instead of a global fp32 load round trip + a chain (round 4's K2s kept ~70 % of its time in
+// those). The cost: a few more entries per list -- those within 2 m_u of the k-th value --
+// which the tight per-user margin keeps small (~k + 9 at C5, d = 64).
+//
+// The item fragments are shared by the block's waves through LDS, as the fragment ring
+// described at the loop; lists live in LDS (CAP entries per user, one per lane).
+// Seeded thresholds. In a streaming top-K most insertions happen early: k ln(N / k) of them
+// over N items, three quarters within the first 1/16 of the range. So a first, screen-only pass
+// (SEEDP) over the first 1/16 of the items keeps, per user, the largest LB of each of C classes
+// of items (item index mod C, C = 16 x the tiles per ring chunk, at most 64), no insertions at
+// all. If E_u of the user's excluded items lie in that range, the (K + E_u)-th largest class
+// maximum s_u is a lower bound of the final K-th value: K + E_u distinct items reach it, at most
+// E_u of them excluded (their final value is the mask value), so K scoring items of the
+// catalog score >= s_u (no seed when K + E_u > C). The main pass never lets a user's entry
+// threshold fall under the float below s_u (unless the mask value is above it: then an
+// excluded item could rank, and everything enters). Several splits: each split's seed is
+// valid on its own, the largest is kept.
+
+// float <-> uint32 with the same order (NaN excluded by the callers)
+__device__ __forceinline__ uint32_t ford(float f) {
+  const uint32_t b = __builtin_bit_cast(uint32_t, f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float funord(uint32_t o) {
+  return __builtin_bit_cast(float, (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+// fl(b - m) nudged down past the subtraction's rounding (<= b - m exactly); fl(b + m) up
+__device__ __forceinline__ float lbound(float b, float m) {
+  const float d = b - m;
+  return d - (fabsf(d) * 0x1p-22f + 1e-30f);
+}
+__device__ __forceinline__ float ubound(float b, float m) {
+  const float e = b + m;
+  return e + (fabsf(e) * 0x1p-22f + 1e-30f);
+}
+
+constexpr uint32_t kFinal = 0x80000000u;  // list entry id bit: the key is the final value
+
+#ifdef LG_TOPK_COUNT  // measurement builds only: event counts of k_topk_ring (lg_topk_counts)
+__device__ unsigned long long g_topk_counts[8];
+#define LG_COUNT(i, v) (cnt_ev[i] += (v))
+#else
+#define LG_COUNT(i, v) ((void)0)
+#endif
+
+template <int D, int NG, int WAVES, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
+__global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
+    const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
+    const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
+    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
+    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
+    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
+    float *__restrict__ part_val, int32_t *__restrict__ part_idx,
+    const float *__restrict__ seed_val) {
+  constexpr int Q = D / 4;   // f32 MFMA steps
+  constexpr int S = D / 32;  // bf16 MFMA k-blocks
+  static_assert(CAP <= 64 && CAP >= 48, "one list entry per lane, room for k + a tile");
+  // the fragment ring: chunks of CI items (8 KiB, one 16-byte LDS-DMA piece per thread)
+  constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D;
+  static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
+  static_assert(LAG >= 1 && LA > LAG && NBUF > LA, "ring shape");
+  // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane)
+  constexpr int TPC_S = TPC < 4 ? TPC : 4;
+  constexpr int NCLS = 16 * TPC_S;
+  // (the seed pass keeps its class maxima in ls instead of lists: no ids)
+  __shared__ float ls[WAVES][NG][16][SEEDP ? NCLS : CAP];
+  __shared__ uint32_t li[WAVES][NG][16][SEEDP ? 1 : CAP];
+  __shared__ int exs[WAVES][64];  // exclusion runs; the exact chain's results
+  __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
+  __shared__ uint32_t arrive[NBUF], done[NBUF];
+
+  const int wave = threadIdx.x / 64;
+  const int lane = lane_id();
+  const int ul = lane & 15;
+  const int gq = lane >> 4;
+  const int64_t tile = blockIdx.x / n_splits;
+  const int split = blockIdx.x % n_splits;
+  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
+  // (waves past the last user still stage their share of every chunk; their users are
+  // invalid, so they never hit the screen and write nothing)
+  const int64_t i0 = (int64_t)split * items_per_split;
+  int64_t i1 = i0 + items_per_split;
+  if (i1 > n_items) i1 = n_items;
+  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;
+  const int n_t = (n_valid + 15) / 16;
+
+  bf16x8 ub[NG][S];
+  float marg[NG];
+  bool uvalid[NG];
+  int64_t ex_pos[NG], ex_hi[NG];
+  int cnt[NG], chk[NG];
+  float thr[NG];
+  float sthr[NG];  // the seeded floor of the threshold (-inf without a seed)
+  // the entry threshold over a list's k-th lower bound tau and the seed floor st: an
+  // excluded item ranks at the mask value, so while that reaches the floor anything enters
+  auto entry_thr = [&](float tau, float st) __attribute__((always_inline)) {
+    const float tf = fmaxf(tau, st);
+    return mask_value > tf ? neg_inf<float>() : tf;
+  };
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int64_t u = ubase + g * 16 + ul;
+    uvalid[g] = u < n_users;
+    const int64_t uu = uvalid[g] ? u : n_users - 1;
+    sthr[g] = neg_inf<float>();
+    if (seed_val && uvalid[g]) {  // (a non-finite seed -- NaN embeddings -- seeds nothing)
+      const float sv = seed_val[u * k + k - 1];
+      if (sv > neg_inf<float>() && sv < __builtin_huge_valf()) sthr[g] = next_below(sv);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
+    marg[g] = umarg[uu];
+    ex_pos[g] = 0;
+    ex_hi[g] = 0;
+    if (ex_rowptr && uvalid[g]) {
+      ex_pos[g] = ex_rowptr[u];
+      ex_hi[g] = ex_rowptr[u + 1];
+    }
+    cnt[g] = 0;
+    chk[g] = 0;
+    thr[g] = uvalid[g] ? entry_thr(neg_inf<float>(), sthr[g]) : __builtin_huge_valf();
+  }
+#ifdef LG_TOPK_COUNT
+  // 0 inserted entries, 1 group-tiles with a hit, 2 compactions, 3 escapes (lists made exact
+  // mid-stream), 4 exclusion-row loads, 5 entries ranked exactly at the end, 6 users finished
+  unsigned long long cnt_ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  const uint64_t same_user = 0x0001000100010001ull << ul;
+  // retire the prologue loads with a wait hipcc sees (vmcnt(0)): otherwise its waitcnt pass
+  // merges their pending state into the loop header, and the screen loop's waits for them
+  // also drained the fragment ring's DMA issued at the chunk start
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+
+  // The exact chain scores of the list entries of user `user` on the lanes in `want` (lane e:
+  // entry e, item `item`): k_score_topk's f32 MFMA chain with 16 entries as the A rows and the
+  // user in every B column, so column ul of the result is the chain of (user, entry) bit for
+  // bit. Results pass through exs (lane e reads its own).
+  auto exact_entries = [&](int64_t user, uint64_t want, int item) __attribute__((always_inline)) {
+    float uf[Q];
+    load_piece<Q>(eu + user * D + gq * Q, uf);
+    constexpr int NB = CAP / 16 + (CAP % 16 ? 1 : 0);  // 16-entry batches
+    constexpr int BL = D <= 64 ? 4 : 2;               // batches whose rows load together
+#pragma unroll
+    for (int b0 = 0; b0 < NB; b0 += BL) {
+      float af[BL][Q];
+#pragma unroll
+      for (int b = 0; b < BL; ++b) {
+        const int e = 16 * (b0 + b) + ul;
+        const int it = __shfl(item, e < 64 ? e : 63);
+        const bool w = b0 + b < NB && e < 64 && ((want >> e) & 1ull);
+        load_piece<Q>(ei + (int64_t)(w ? it : 0) * D + gq * Q, af[b]);
+      }
+#pragma unroll
+      for (int b = 0; b < BL; ++b) {
+        if (b0 + b >= NB || ((want >> (16 * (b0 + b))) & 0xffffull) == 0) continue;  // (uniform)
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < Q; ++s)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[b][s], uf[s], acc, 0, 0, 0);
+        // rows 4 gq + r of column ul: every column holds the same user
+        if (ul == 0)
+          *reinterpret_cast<f32x4 *>(&exs[wave][16 * (b0 + b) + 4 * gq]) = acc;
+      }
+    }
+    wave_sync();
+    const float raw = __builtin_bit_cast(float, exs[wave][lane]);
+    wave_sync();
+    return raw;
+  };
+
+  // Compaction of user u of group g (the whole wave; lane e holds entry e). (1) The lazy
+  // exclusion of k_score_topk: the entries [chk, n) added since the last compaction lie in
+  // [previous limit, lim) and the user's excluded items there are the next run of its sorted
+  // exclusion row; an excluded entry takes the mask value as its final value. (2) tau = the
+  // k-th largest LB (radix select over ballots); entries with UB below max(tau, seed floor)
+  // go. (3) With `fin` (the end of the stream), or when more entries remain than leave room
+  // for a tile, the rest get their exact chain scores: entries whose score is NaN or -inf go
+  // (k_score_topk never inserts them), the others are sorted (value desc, item asc) and the
+  // best k kept, all final. Returns, on lane e < k, the e-th output entry when fin.
+  // (g is a run-time, wave-uniform group index: the loop has one compaction site, not one
+  // per group and tile -- inlined copies made the kernel ~54 KB of code)
+  auto gget = [&](const auto (&a)[NG], int g) __attribute__((always_inline)) {
+    auto v = a[0];
+#pragma unroll
+    for (int j = 1; j < NG; ++j)
+      if (g == j) v = a[j];
+    return v;
+  };
+  auto compact_user = [&](int g, int u, int lim, bool fin, float &ov, int &oi)
+      __attribute__((always_inline)) {
+    const int n = __shfl(gget(cnt, g), u);
+    const int c0 = __shfl(gget(chk, g), u);
+    int64_t pos = __shfl(gget(ex_pos, g), u);
+    const int64_t hi = __shfl(gget(ex_hi, g), u);
+    const float m = __shfl(gget(marg, g), u), st = __shfl(gget(sthr, g), u);
+    float *ks = &ls[wave][g][u][0];
+    uint32_t *is = &li[wave][g][u][0];
+    if (n > c0) {
+      while (pos < hi) {
+        const int64_t e = pos + lane;
+        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
+        LG_COUNT(4, 1);
+        const int nin = __popcll(__ballot(x < lim));  // ascending: a prefix of the lanes
+        if (nin == 0) break;
+        exs[wave][lane] = x;
+        wave_sync();
+        if (lane >= c0 && lane < n) {
+          const int item = (int)is[lane];  // (entries since the last compaction: not final)
+          int a = 0, b = nin;              // first index with exs[] >= item
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (exs[wave][mid] < item) a = mid + 1;
+            else b = mid;
+          }
+          if (a < nin && exs[wave][a] == item) {
+            ks[lane] = mask_value;
+            is[lane] = (uint32_t)item | kFinal;
+          }
+        }
+        wave_sync();
+        pos += nin;
+        if (nin < 64) break;
+      }
+    }
+    const bool have = lane < n;
+    const float key = have ? ks[lane] : 0.f;
+    const uint32_t idr = have ? is[lane] : 0u;
+    const bool isfin = (idr & kFinal) != 0;
+    const int item = (int)(idr & ~kFinal);
+    float lb = isfin ? key : lbound(key, m);
+    float hb = isfin ? key : ubound(key, m);
+    lb = lb == lb ? lb : neg_inf<float>();           // (NaN: no lower bound)
+    hb = hb == hb ? hb : __builtin_huge_valf();      // (NaN: no upper bound)
+    float tau = neg_inf<float>();
+    if (n >= k) {  // the k-th largest LB: greatest T with k lanes at or above it
+      const uint32_t o = ford(lb);
+      uint32_t T = 0u;
+#pragma unroll 4
+      for (int b = 31; b >= 0; --b) {
+        const uint32_t c = T | (1u << b);
+        if (__popcll(__ballot(have && o >= c)) >= k) T = c;
+      }
+      tau = funord(T);
+    }
+    const bool keep = have && hb >= fmaxf(tau, st);
+    const uint64_t kb = __ballot(keep);
+    int nk = __popcll(kb);
+    wave_sync();  // (every lane has read its entry)
+    LG_COUNT(2, fin ? 0 : 1);
+    LG_COUNT(3, (!fin && nk > CAP - 16) ? 1 : 0);
+    LG_COUNT(5, fin ? nk : 0);
+    LG_COUNT(6, fin ? 1 : 0);
+    if (fin || nk > CAP - 16) {
+      const float raw = exact_entries(ubase + g * 16 + u, kb, item);
+      const bool ok = keep && raw == raw && raw > neg_inf<float>();
+      float kk[1] = {ok ? (isfin ? key : raw) : neg_inf<float>()};
+      int ii[1] = {ok ? item : kPadId};
+      wave_bitonic_sort<float, 1>(kk, ii);
+      nk = __popcll(__ballot(ok));
+      nk = nk < k ? nk : k;
+      if (lane < nk) {
+        ks[lane] = kk[0];
+        is[lane] = (uint32_t)ii[0] | kFinal;
+      }
+      tau = nk == k ? __shfl(kk[0], k - 1) : neg_inf<float>();
+      ov = lane < nk ? kk[0] : neg_inf<float>();
+      oi = lane < nk ? ii[0] : -1;
+    } else if (keep) {
+      const int p = __popcll(kb & lanemask_lt());
+      ks[p] = key;
+      is[p] = idr;
+    }
+    wave_sync();
+    const float nthr = entry_thr(tau, st);
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+      if (j == g && ul == u) {
+        cnt[j] = nk;
+        chk[j] = nk;
+        ex_pos[j] = pos;
+        thr[j] = uvalid[j] ? nthr : __builtin_huge_valf();
+      }
+  };
+  // compact every list that could overflow on the next tile (+16 entries max per tile)
+  auto compact_over = [&](int lim) __attribute__((always_inline)) {
+    uint32_t need = 0;  // bit 16 g + u
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      need |= (uint32_t)(__ballot(cnt[g] > CAP - 16) & 0xffffull) << (16 * g);
+    wave_sync();
+    while (need) {
+      const int b = __builtin_ctz(need);
+      need &= need - 1;
+      float ov;
+      int oi;
+      compact_user(b >> 4, b & 15, lim, false, ov, oi);
+    }
+  };
+  // insertion of group g's bf16 products accb of tile t (lane (ul, gq): items 4 gq + r of the
+  // tile, user ul): every item whose upper bound beats the running threshold enters with its
+  // product as the key
+  auto insert_bound = [&](int t, int g, const f32x4 acc) __attribute__((always_inline)) {
+    const int rel = t * 16 + gq * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool cand = rel + r < n_valid && above(acc[r] + marg[g], thr[g]);
+      const uint64_t bal = __ballot(cand);
+      LG_COUNT(0, __popcll(bal));
+      if (bal) {
+        const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
+        if (cand) {
+          ls[wave][g][ul][pos] = acc[r];
+          li[wave][g][ul][pos] = (uint32_t)((int)i0 + rel + r);
+        }
+        cnt[g] += __popcll(bal & same_user);
+      }
+    }
   };
 
   const int lim_end = (int)i1;
-  // tile t: the bf16 screen of its fragments fr, then (rarely) the exact tile and compaction
-  auto screen_tile = [&](int t, const bf16x8 (&fr)[S], auto &&after_mfma)
-      __attribute__((always_inline)) {
-    f32x4 accb[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s], ub[g][s], accb[g], 0, 0, 0);
-    }
-    after_mfma();
-    bool gh[NG];
-    bool hit = false;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
-      gh[g] = __ballot(above(max4(accb[g]) + marg[g], thr[g])) != 0;
-      hit |= gh[g];
-    }
-    if (hit) {
-      exact_tile(t, gh);
-      const int l = (int)i0 + (t + 1) * 16;
-      maybe_compact(l < lim_end ? l : lim_end);
-    }
-  };
   // the seed pass's class maxima (SEEDP only)
   f32x4 cmax[NG][SEEDP ? TPC_S : 1];
 #pragma unroll
@@ -604,16 +917,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     for (int tt = 0; tt < (SEEDP ? TPC_S : 1); ++tt)
       cmax[g][tt] = f32x4{neg_inf<float>(), neg_inf<float>(), neg_inf<float>(),
                           neg_inf<float>()};
-  if constexpr (SH) {
+  {
     // The block's waves share the bf16 item fragments through LDS: chunks of CI items (8 KiB,
     // one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a ring of
     // NBUF buffers; the 16-byte pieces of row r stored XOR-swizzled by sw(r) through the
     // SOURCE address, so the fragment reads of any 16 consecutive lanes hit distinct banks
     // (the layout of csrc/gbound.hip).
-    // No block barrier per chunk: an exact tile (a global load round trip, the fp32 chain, the
-    // insertion) holds one wave for several chunks' worth of screening, and a barrier made
-    // every wave wait for the slowest one each chunk. Instead the waves drift up to 3 chunks
-    // apart, coupled by two LDS counters per buffer:
+    // No block barrier per chunk: the waves drift apart, coupled by two LDS counters per
+    // buffer:
     //   arrive[b]: +1 per wave once its piece of the chunk in b has landed (its own vmcnt);
     //   done[b]:   +1 per wave once it has read the chunk in b.
     // Wave w at chunk c: (1) once every wave is done with chunk c + LA - NBUF, issue its piece
@@ -621,24 +932,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     // have landed -- and signal arrival for chunk c + LA - LAG; (3) wait until all WAVES
     // pieces of chunk c have arrived; (4) screen it; (5) signal done. The slowest wave never
     // waits (the others are past the chunks it needs them for), so the ring cannot deadlock; a
-    // wave is at most min(LA - LAG, NBUF - LA) chunks ahead of the slowest. The DMA is inline asm with no register
-    // outputs, invisible to hipcc's waits (hipcc's own __builtin_amdgcn_global_load_lds puts
-    // vmcnt(0) before every LDS read, as it cannot tell the ring's buffers apart); an
-    // untracked load only makes hipcc's own vmcnt waits stricter (the counter retires in
-    // order).
-    constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D;
-#ifndef LG_RING_NBUF  // (measurement builds may override the ring shape: -DLG_RING_NBUF=...)
-#define LG_RING_NBUF 7
-#define LG_RING_LA 4
-#define LG_RING_LAG 1
-#endif
-    // ring buffers; chunks a wave issues ahead of its own; chunks between a piece's issue and
-    // its arrival signal
-    constexpr int NBUF = LG_RING_NBUF, LA = LG_RING_LA, LAG = LG_RING_LAG;
-    static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
-    static_assert(LAG >= 1 && LA > LAG && NBUF > LA, "ring shape");
-    __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
-    __shared__ uint32_t arrive[NBUF], done[NBUF];
+    // wave is at most min(LA - LAG, NBUF - LA) chunks ahead of the slowest. The DMA is inline
+    // asm with no register outputs, invisible to hipcc's waits (hipcc's own
+    // __builtin_amdgcn_global_load_lds puts vmcnt(0) before every LDS read, as it cannot tell
+    // the ring's buffers apart); an untracked load only makes hipcc's own vmcnt waits stricter
+    // (the counter retires in order).
     auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
     const int pp = (int)threadIdx.x, pr = pp / PR;
     const int pcol = 8 * ((pp % PR) ^ sw(pr));
@@ -673,6 +971,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG) : "memory");
     for (int c = 0; c < LA - LAG; ++c) signal(&arrive[c]);
     for (int c = 0; c < n_c; ++c) {
+#ifndef LG_RING_PROBE_NORING  // (measurement builds: no ring protocol, chunk 0's buffer reread)
       {
         const int cn = c + LA, cp = cn - NBUF;  // chunk cn replaces chunk cp in its buffer
         if (cp >= 0) wait_for(&done[cp % NBUF], (uint32_t)(WAVES * (cp / NBUF + 1)));
@@ -682,14 +981,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       }
       wait_for(&arrive[c % NBUF], (uint32_t)(WAVES * (c / NBUF + 1)));
       const char *fb = frs[c % NBUF];
+#else
+      const char *fb = frs[0];
+#endif
       const int t0 = c * TPC;
       // The chunk's TPC tiles are screened together -- every fragment read, then every bf16
       // MFMA, then the hit tests -- so the reads and the MFMA chains of different tiles
       // overlap instead of one tile's LDS -> MFMA -> compare chain at a time. The tests use
       // the thresholds of the chunk start: never above the running ones (they only rise), so
-      // a tile they rule out holds no score that could enter later either. (Deferring the
-      // exact tiles by one chunk, so their fp32 loads overlap the next chunk's screen, was
-      // measured slower: 20.7 vs 17.9 ms at C5, d = 64, with a barrier per chunk.)
+      // a tile they rule out holds no item that could enter later either.
       bf16x8 fr[TPC][S];
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt) {
@@ -710,11 +1010,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
             accb[tt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[tt][s], ub[g][s],
                                                                   accb[tt][g], 0, 0, 0);
         }
+#ifndef LG_RING_PROBE_NORING
       signal(&done[c % NBUF]);  // (the fragments are in registers: the buffer is free)
+#endif
       if constexpr (SEEDP) {
-        // the seed pass: each lane's running maxima of the lower bounds fl(bf16 product - m_u)
-        // (nudged down past the subtraction's rounding; past the range: -inf; a NaN stays NaN
-        // and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
+        // the seed pass: each lane's running maxima of the lower bounds (past the range: -inf;
+        // a NaN stays NaN and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
 #pragma unroll
         for (int tt = 0; tt < TPC; ++tt) {
           const int rel = (t0 + tt) * 16 + gq * 4;
@@ -722,8 +1023,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
           for (int g = 0; g < NG; ++g)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float d = accb[tt][g][r] - marg[g];
-              const float lb = rel + r < n_valid ? d - (fabsf(d) * 0x1p-22f + 1e-30f)
+              const float lb = rel + r < n_valid ? lbound(accb[tt][g][r], marg[g])
                                                  : neg_inf<float>();
               cmax[g][tt % TPC_S][r] = __builtin_elementwise_maximum(cmax[g][tt % TPC_S][r], lb);
             }
@@ -735,76 +1035,61 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
       for (int tt = 0; tt < TPC; ++tt)
 #pragma unroll
         for (int g = 0; g < NG; ++g)
-          // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
-          if (__ballot(above(max4(accb[tt][g]) + marg[g], thr[g])) != 0 && t0 + tt < n_t)
+          // (a NaN bound, e.g. from a non-finite embedding or margin, enters)
+          if (__ballot(above(max4(accb[tt][g]) + marg[g], thr[g])) != 0)
             hits |= 1u << (tt * NG + g);
-#ifdef LG_SCREEN_PROBE  // measurement builds only (wrong lists): 1 = screen alone, 2 = all exact
-      hits = LG_SCREEN_PROBE == 1 ? 0u : (t0 + TPC <= n_t ? (1u << (TPC * NG)) - 1u : hits);
+      if (t0 + TPC > n_t) hits &= (1u << ((n_t - t0) * NG)) - 1u;  // (tiles past the split)
+#ifdef LG_SCREEN_PROBE  // measurement builds only (wrong lists): the screen and its tests alone
+      asm volatile("" ::"s"(hits));
+      hits = 0u;
 #endif
-#ifndef LG_EXACT_BATCH  // (1: measured slower, 15.0 vs 13.9 ms at C5, d = 64)
-#define LG_EXACT_BATCH 0
-#endif
-      if constexpr (LG_EXACT_BATCH && D <= 64) {
-        // the fp32 fragments of every hit tile of the chunk are loaded together (one load
-        // round trip for the chunk's exact tiles: all of them while the thresholds warm up),
-        // then the tiles run in order
-        float afc[TPC][Q];
+      if (hits == 0) continue;  // (the common case: one branch)
+      // The hit tiles in order; when a list could overflow on the next tile, the lists are
+      // compacted (one code site) and the insertion resumes after that tile. The bf16
+      // products pass an opaque (empty) asm first: otherwise hipcc hoists the insertion's
+      // set-up -- 32 bound sums, item ids, range tests, SGPR spills -- out of this rare path
+      // into every chunk (~150 VALU per chunk measured).
 #pragma unroll
-        for (int tt = 0; tt < TPC; ++tt)
-          if ((hits >> (tt * NG)) & ((1u << NG) - 1u)) load_exact(t0 + tt, afc[tt]);
+      for (int tt = 0; tt < TPC; ++tt)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) asm volatile("" : "+v"(accb[tt][g]));
+      int tt0 = 0;
+      while (hits) {
+        int stop = TPC;
 #pragma unroll
         for (int tt = 0; tt < TPC; ++tt) {
-          if (((hits >> (tt * NG)) & ((1u << NG) - 1u)) == 0) continue;  // (wave-uniform)
-          bool gh[NG];
+          const uint32_t th = (hits >> (tt * NG)) & ((1u << NG) - 1u);
+          if (tt < tt0 || stop != TPC || th == 0) continue;  // (wave-uniform)
+          LG_COUNT(1, __popc(th));
 #pragma unroll
-          for (int g = 0; g < NG; ++g) gh[g] = (hits >> (tt * NG + g)) & 1u;
-          exact_from(t0 + tt, gh, afc[tt]);
-          const int l = (int)i0 + (t0 + tt + 1) * 16;
-          maybe_compact(l < lim_end ? l : lim_end);
-        }
-      } else {
-        while (hits) {
-          const int tt = (__builtin_ctz(hits)) / NG;
-          bool gh[NG];
+          for (int g = 0; g < NG; ++g)
+            if ((th >> g) & 1u) insert_bound(t0 + tt, g, accb[tt][g]);
+          bool over = false;
 #pragma unroll
-          for (int g = 0; g < NG; ++g) gh[g] = (hits >> (tt * NG + g)) & 1u;
-          hits &= ~(((1u << NG) - 1u) << (tt * NG));
-          exact_tile(t0 + tt, gh);
-          const int l = (int)i0 + (t0 + tt + 1) * 16;
-          maybe_compact(l < lim_end ? l : lim_end);
+          for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
+          if (__ballot(over) != 0) stop = tt;
         }
+        if (stop == TPC) break;
+        const int l = (int)i0 + (t0 + stop + 1) * 16;
+        compact_over(l < lim_end ? l : lim_end);
+        tt0 = stop + 1;
+        hits &= ~((1u << (tt0 * NG)) - 1u);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA in flight at the exit)
-  } else {
-    // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
-    // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
-    // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at
-    // C5, d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
-    bf16x8 fr[2][S];
-    load_bf(0, fr[0]);
-    load_bf(1, fr[1]);
-    for (int t0 = 0; t0 < n_t; t0 += 2) {
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int t = t0 + p;
-        if (t >= n_t) break;
-        // tile t + 2 into the buffer tile t just left, right after tile t's MFMAs
-        screen_tile(t, fr[p], [&] { load_bf(t + 2, fr[p]); });
-      }
-    }
   }
 
   wave_sync();
   if constexpr (SEEDP) {
     // per user: the (k + E)-th largest of its NCLS class maxima (E = its excluded items in this
-    // split's range), into the K-th slot of its output row; -inf when k + E > NCLS
+    // split's range, by two binary searches of its sorted exclusion row), into the K-th slot of
+    // its output row; -inf when k + E > NCLS
 #pragma unroll
     for (int g = 0; g < NG; ++g)
 #pragma unroll
       for (int tt = 0; tt < TPC_S; ++tt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cs[wave][g][ul][16 * tt + 4 * gq + r] = cmax[g][tt][r];
+        for (int r = 0; r < 4; ++r) ls[wave][g][ul][16 * tt + 4 * gq + r] = cmax[g][tt][r];
     wave_sync();
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -813,19 +1098,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
         if (user >= n_users) break;
         int E = 0;
         if (ex_rowptr) {
-          const int64_t e1 = ex_rowptr[user + 1];
-          for (int64_t e = ex_rowptr[user] + lane; __ballot(e < e1) != 0; e += 64) {
-            const int32_t x = e < e1 ? ex_col[e] : -1;
-            E += __popcll(__ballot(x >= i0 && x < i1));
-          }
+          const int64_t e0 = ex_rowptr[user], e1 = ex_rowptr[user + 1];
+          E = (int)(lower_bound_i32(ex_col, e0, e1, (int32_t)i1) -
+                    lower_bound_i32(ex_col, e0, e1, (int32_t)i0));
         }
         const int need = k + E;  // (wave-uniform)
         float sv = neg_inf<float>();
         if (need <= NCLS) {
-          const float v = lane < NCLS ? cs[wave][g][u][lane] : neg_inf<float>();
+          const float v = lane < NCLS ? ls[wave][g][u][lane] : neg_inf<float>();
           int rank = 0;  // entries above v, ties by class index
           for (int j = 0; j < NCLS; ++j) {
-            const float w = cs[wave][g][u][j];
+            const float w = ls[wave][g][u][j];
             rank += (w > v || (w == v && j < lane)) ? 1 : 0;
           }
           const uint64_t b = __ballot(lane < NCLS && rank == need - 1);
@@ -839,28 +1122,32 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
     }
     return;
   }
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    for (int u = 0; u < 16; ++u) {
-      const int64_t user = ubase + g * 16 + u;
+#pragma unroll 1
+  for (int b = 0; b < 16 * NG; ++b) {  // (user ubase + b = group b / 16, column b % 16)
+    {
+      const int64_t user = ubase + b;
       if (user >= n_users) break;
-      compact_user(g, u, lim_end);
-      const int nc = __shfl(cnt[g], u);
-      for (int e = lane; e < k; e += 64) {
-        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
-        const int id = e < nc ? ci[wave][g][u][e] : -1;
+      float v;
+      int id;
+      compact_user(b >> 4, b & 15, lim_end, true, v, id);
+      if (lane < k) {
         if (n_splits == 1) {
-          out_val[user * k + e] = v;
-          out_idx[user * k + e] = id;
+          out_val[user * k + lane] = v;
+          out_idx[user * k + lane] = id;
         } else {
-          const int64_t o = ((int64_t)split * n_users + user) * k + e;
+          const int64_t o = ((int64_t)split * n_users + user) * k + lane;
           part_val[o] = v;
           part_idx[o] = id;
         }
       }
-      wave_sync();
     }
   }
+#ifdef LG_TOPK_COUNT
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i)
+      if (cnt_ev[i]) __hip_atomic_fetch_add(&g_topk_counts[i], cnt_ev[i], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
@@ -1047,6 +1334,22 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
   out_val[u * k + k - 1] = m;
 }
 
+// the k <= 32 ring kernel's shape: list capacity, fragment-ring buffers, chunks a wave issues
+// ahead, chunks between a piece's issue and its arrival signal (measurement builds may
+// override them: -DLG_RING_CAP=... etc.)
+#ifndef LG_RING_CAP
+#define LG_RING_CAP 56
+#endif
+#ifndef LG_RING_NBUF
+#define LG_RING_NBUF 5
+#endif
+#ifndef LG_RING_LA
+#define LG_RING_LA 3
+#endif
+#ifndef LG_RING_LAG
+#define LG_RING_LAG 1
+#endif
+
 template <int D>
 static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float *ei,
                                  const __bf16 *eub, const __bf16 *eib, const float *umarg,
@@ -1055,21 +1358,30 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
                                  float *part_val, int32_t *part_idx, const float *seed_val,
                                  hipStream_t stream) {
-#define LG_SCREEN_LAUNCH(NG, MM, W, SH, SEEDP)                                                 \
+#define LG_SCREEN_LAUNCH(NG, MM, W)                                                           \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_score_topk_screen<D, NG, MM, W, SH, SEEDP>                                              \
+    k_score_topk_screen<D, NG, MM, W>                                                         \
         <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
+            eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
+            n_splits, items_per_split, out_val, out_idx, part_val, part_idx);                 \
+  }
+  // k <= 32: one 8-wave block per CU (RING_CAP-entry lists for 256 users + the fragment
+  // ring) shares the item fragments; larger lists keep 2-wave blocks that load their own
+#define LG_RING_LAUNCH(SEEDP)                                                                 \
+  {                                                                                           \
+    const int64_t tiles = (n_users + 255) / 256;                                              \
+    k_topk_ring<D, 2, 8, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, LG_RING_LAG, SEEDP>           \
+        <<<dim3((unsigned)(tiles * n_splits)), dim3(512), 0, stream>>>(                       \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
-  // k <= 32: one 8-wave block per CU (128 KiB of lists + the 24 KiB fragment ring) shares
-  // the item fragments; larger lists keep 2-wave blocks that load their own
-  if (M == 1 && seedp) LG_SCREEN_LAUNCH(2, 1, 8, true, true)
-  else if (M == 1) LG_SCREEN_LAUNCH(2, 1, 8, true, false)
-  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2, false, false)
-  else LG_SCREEN_LAUNCH(1, 4, 2, false, false)
+  if (M == 1 && seedp) LG_RING_LAUNCH(true)
+  else if (M == 1) LG_RING_LAUNCH(false)
+  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2)
+  else LG_SCREEN_LAUNCH(1, 4, 2)
+#undef LG_RING_LAUNCH
 #undef LG_SCREEN_LAUNCH
 }
 
@@ -1238,3 +1550,14 @@ extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_us
   }
   return launch_status("lg_score_dense_f32");
 }
+
+#ifdef LG_TOPK_COUNT
+// measurement builds only: read and clear k_topk_ring's event counts (8 x uint64, host)
+extern "C" int lg_topk_counts(unsigned long long *host8) {
+  if (hipDeviceSynchronize() != hipSuccess) return LG_ERR_HIP;
+  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_topk_counts), 64) != hipSuccess) return LG_ERR_HIP;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_topk_counts), z, 64) != hipSuccess) return LG_ERR_HIP;
+  return LG_OK;
+}
+#endif

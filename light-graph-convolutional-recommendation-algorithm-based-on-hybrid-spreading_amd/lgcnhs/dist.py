@@ -24,6 +24,7 @@ The per-shard layer is pluggable so the bookkeeping can run on CPU with gloo
 from __future__ import annotations
 
 import math
+import time
 
 import torch
 import torch.distributed as dist
@@ -176,6 +177,47 @@ def _gather_block(buf: torch.Tensor, shard: RowShard, c: int, group=None, async_
     return dist.all_gather_into_tensor(blk, mine, group=group, async_op=async_op)
 
 
+class _WaitTimer:
+    """Times one batch of gather waits into `log` (a list, or None: no timing) as
+    (layer, interval). On a GPU the wait is a stream-side dependency (Work.wait() makes the
+    compute stream wait for RCCL's), so the interval is a pair of events recorded on the
+    compute stream around it: their distance is how long that stream stalled on the
+    exchange, i.e. the part of the gather the overlap did not hide (elapsed_time, ms). On
+    the CPU (gloo) wait() blocks the host: host seconds."""
+
+    def __init__(self, log, layer, like):
+        self.log, self.layer = log, layer
+        self.cuda = like is not None and like.is_cuda
+
+    def __enter__(self):
+        if self.log is not None:
+            if self.cuda:
+                self.a = torch.cuda.Event(enable_timing=True)
+                self.a.record()
+            else:
+                self.t = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        if self.log is not None:
+            if self.cuda:
+                b = torch.cuda.Event(enable_timing=True)
+                b.record()
+                self.log.append((self.layer, (self.a, b)))
+            else:
+                self.log.append((self.layer, (time.perf_counter() - self.t) * 1e3))
+        return False
+
+
+def exposed_wait_ms(waits, layers: int, steps: int) -> list:
+    """Per layer, the mean over `steps` forwards of the compute stream's stall on the gathers
+    (ms; from BipartitePropagation.waits / ShardedPropagation.waits after a synchronize)."""
+    per = [0.0] * layers
+    for layer, iv in waits:
+        per[layer] += iv[0].elapsed_time(iv[1]) if isinstance(iv, tuple) else float(iv)
+    return [v / max(steps, 1) for v in per]
+
+
 class ShardedPropagation:
     """mean_{l<=L} A_hat^l e0 on this rank's rows, all-gathers overlapped with the SpMM."""
 
@@ -188,6 +230,7 @@ class ShardedPropagation:
                      torch.zeros(n_pad, dim, device=device) if layers > 2 else None]
         self.out = torch.zeros(n_pad, dim, device=device)
         self.events = None  # optional list of (start, end) event pairs around each layer
+        self.waits = None  # optional list of (layer, interval): the stall on the gathers
 
     def forward(self, e0_layout: torch.Tensor, gather_out: bool = False) -> torch.Tensor:
         """e0_layout: [n_pad, d] layer-0 embeddings in the chunk-major layout (replicated).
@@ -213,8 +256,9 @@ class ShardedPropagation:
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 self.events.append((s, e))
-            for h in handles:
-                h.wait()
+            with _WaitTimer(self.waits, l, y):
+                for h in handles:
+                    h.wait()
             x = y
         if gather_out and sh.world > 1:
             for c in range(sh.chunks):
@@ -358,6 +402,9 @@ class BipartitePropagation:
         self.out = torch.zeros(n_pad, dim, device=device)
         self.bipartite = shard.is_bipartite()
         self.events = None  # optional list of (start, end) event pairs: one per layer half
+        # optional list of (layer, interval) -- the compute stream's stall on the gathers it
+        # awaits before each half (see _WaitTimer): the exchange the overlap did NOT hide
+        self.waits = None
 
     def forward(self, e0_layout: torch.Tensor, gather_out: bool = False) -> torch.Tensor:
         sh = self.shard
@@ -373,9 +420,10 @@ class BipartitePropagation:
             fresh = {}
             for s in order:
                 need = [1 - s] if (self.bipartite and nseg == 2) else list(pending)
-                for q in need:
-                    for h in pending.pop(q, []):
-                        h.wait()
+                with _WaitTimer(self.waits, l, x):
+                    for q in need:
+                        for h in pending.pop(q, []):
+                            h.wait()
                 if self.events is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev0.record()
@@ -388,9 +436,10 @@ class BipartitePropagation:
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record()
                     self.events.append((ev0, ev1))
-            for hs in pending.values():  # (non-bipartite leftovers)
-                for h in hs:
-                    h.wait()
+            with _WaitTimer(self.waits, l, x):
+                for hs in pending.values():  # (non-bipartite leftovers)
+                    for h in hs:
+                        h.wait()
             pending = fresh
             x = y
         if gather_out and sh.world > 1:

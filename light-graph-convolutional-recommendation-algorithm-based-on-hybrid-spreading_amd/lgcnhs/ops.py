@@ -203,9 +203,37 @@ def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512,
 
 
 # |bf16 MFMA product - fp32 chain| <= 0.00785 ||u|| ||i|| (csrc/gbound.hip); 3 % slack for
-# the fp32 roundings of the margin and of the screen's compare
+# the fp32 roundings of the margin and of the screen's compare. The worst case of bf16
+# rounding; the screened top-K uses the tighter screen_margins (below), this form remains the
+# bound of lg_score_chunk_bound.
 SCREEN_MARGIN = 0.0081
 SCREEN_DEFAULT = True  # measured: 26.8 vs 31.9 ms (d=64), 45.8 vs 59.7 ms (d=128) at C5
+
+
+def screen_margins(un: torch.Tensor, ue: torch.Tensor, inorm: torch.Tensor,
+                   ierr: torch.Tensor, dim: int) -> torch.Tensor:
+    """Per-user fp32 margins m_u >= |bf16 MFMA product - fp32 chain score| for every item
+    (the contract of lg_score_topk_screened_f32's umarg, include/lgcnhs.h).
+
+    With du = u - bf16(u) and di = i - bf16(i) (both exact in fp32):
+      u.i - bf16(u).bf16(i) = du.i + bf16(u).di, so |.| <= ||du|| ||i|| + (||u|| + ||du||) ||di||
+    (Cauchy-Schwarz, ||bf16(u)|| <= ||u|| + ||du||); the MFMA's and the chain's fp32
+    accumulations add gamma_dim (||bf16(u)|| ||bf16(i)|| + ||u|| ||i||) <= 2.01 dim 2^-24 ||u|| ||i||,
+    and 2^-22 ||u|| ||i|| covers the rounding of the screen's own fp32 sum fl(b + m_u) (|b + m_u|
+    <= 1.02 ||u|| ||i||). With I = max ||i||, DI = max ||di|| (norms rounded up by
+    lg_bound_prep_f32), times (1 + 2^-20), plus 1e-30 for flushed subnormal products, in fp64,
+    rounded up to fp32. On N(0, 0.1^2) embeddings this is ~0.45x the worst-case 0.0081 ||u|| I
+    of SCREEN_MARGIN (bf16 rounding errors are not all at their maximum), and the observed
+    error stays below 0.37 of it. Non-finite norms give non-finite margins: the kernel then
+    keeps every item of those users."""
+    I = inorm.max().double()
+    DI = ierr.max().double()
+    u, e = un.double(), ue.double()
+    m = (e * I + (u + e) * DI + (2.01 * dim * 2.0 ** -24 + 2.0 ** -22) * u * I) \
+        * (1.0 + 2.0 ** -20) + 1e-30
+    m32 = m.float()
+    return torch.where(m32.double() < m, torch.nextafter(m32, torch.full_like(m32, float("inf"))),
+                       m32)
 
 
 def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None = None,
@@ -234,11 +262,11 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     ex_rp = N.ptr(excl.rowptr if excl else None)
     ex_c = N.ptr(excl.col if excl else None)
     if screen and nu > 0:
-        ub, un = bound_operands(eu)
-        ib, inorm = bound_operands(ei)
-        # (a non-finite embedding makes a margin NaN or inf: the kernel then recomputes every
-        # tile of those users exactly, so the lists stay lg_score_topk_f32's)
-        umarg = un * (inorm.max() * SCREEN_MARGIN)
+        ub, un, ue = bound_operands(eu, with_err=True)
+        ib, inorm, ierr = bound_operands(ei, with_err=True)
+        # (a non-finite embedding makes a margin NaN or inf: the kernel then keeps every item
+        # of those users and ranks them exactly, so the lists stay lg_score_topk_f32's)
+        umarg = screen_margins(un, ue, inorm, ierr, d)
         N.check(N.lib().lg_score_topk_screened_f32(
             N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d, ex_rp, ex_c,
             float(mask_value), int(k), ns, N.ptr(val), N.ptr(idx), N.ptr(ws), ws_bytes,
@@ -760,15 +788,18 @@ def tile_traffic(A: Interactions, tile: int = 2048, users: slice | None = None,
     return int(tw.paths_read), int(tw.bytes_read)
 
 
-def bound_operands(x: torch.Tensor):
+def bound_operands(x: torch.Tensor, with_err: bool = False):
     """(bf16 copy as int16 storage, fp32 row norms rounded up) of an fp32 [n, d] matrix:
-    the operands of lg_score_chunk_bound."""
+    the operands of lg_score_chunk_bound; with_err also the rounded-up norms of
+    x - bf16(x) (screen_margins' operand)."""
     x = _f32(x, "x")
     xb = torch.empty(x.shape, dtype=torch.int16, device=x.device)
     nrm = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    err = torch.empty(x.shape[0], dtype=torch.float32, device=x.device) if with_err else None
     N.check(N.lib().lg_bound_prep_f32(N.ptr(x), x.shape[0], x.shape[1], N.ptr(xb), N.ptr(nrm),
-                                      N.stream_handle(x.device)), "lg_bound_prep_f32")
-    return xb, nrm
+                                      N.ptr(err), N.stream_handle(x.device)),
+            "lg_bound_prep_f32")
+    return (xb, nrm, err) if with_err else (xb, nrm)
 
 
 def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
@@ -776,7 +807,8 @@ def chunk_bounds(ub, un, ib, inorm, dim: int, j0: int, width: int,
     """[users, ceil(width/64)] fp32 upper bounds of the fp32 score chain over each 64-column
     chunk of items [j0, j0 + width) (lg_score_chunk_bound); with qout ([users, qstride]
     uint8, qstride >= width rounded up to 256) also the per-column 8-bit bounds. Returns gb,
-    or (gb, q) with qout."""
+    or (gb, q) with qout. width <= 4096 (LG_BOUND_MAX_WIDTH; the library refuses wider
+    tiles)."""
     n = ub.shape[0]
     nch = -(-width // 64)
     if out is None or out.numel() < n * nch:

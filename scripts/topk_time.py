@@ -1,4 +1,4 @@
-"""Time ops.score_topk over the C5 catalog (1M items, 32768 users, k=20, e0 ~ N(0, 0.1^2)):
+"""Time ops.score_topk over the C5 catalog (1M items, 32768 users, k=20 (--k), e0 ~ N(0, 0.1^2)):
 the bf16-screened kernel against the plain fp32-MFMA one, lists compared bit for bit.
   --dims 64,128   embedding widths       --modes screen,plain   kernels
   --splits auto,1 item splits            --reps 3               timed calls per case"""
@@ -20,21 +20,27 @@ ap.add_argument("--modes", default="screen,plain")
 ap.add_argument("--splits", default="auto,1")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--users", type=int, default=32768)
-ap.add_argument("--margin-scale", type=float, default=1.0,
-                help="measurement only: scale the screen margin (below 1 it is no longer a "
-                     "proven bound; lists may differ)")
+ap.add_argument("--k", type=int, default=20)
+ap.add_argument("--no-excl", action="store_true", help="no exclusion sets")
 args = ap.parse_args()
-ops.SCREEN_MARGIN *= args.margin_scale
+import ctypes  # noqa: E402
+from lgcnhs import _native as NV  # noqa: E402
+_lib = NV.lib()
+counts = getattr(_lib, "lg_topk_counts", None)  # (measurement builds with -DLG_TOPK_COUNT)
+if counts is not None:
+    counts.argtypes, counts.restype = [ctypes.c_void_p], ctypes.c_int
+    _buf = (ctypes.c_ulonglong * 8)()
+    counts(_buf)
 
 dev = torch.device("cuda:0")
-U, I, k = args.users, 1_000_000, 20
+U, I, k = args.users, 1_000_000, args.k
 for D in [int(x) for x in args.dims.split(",")]:
     g = torch.Generator(device=dev).manual_seed(42)
     eu = torch.randn(U, D, device=dev, generator=g) * 0.1
     ei = torch.randn(I, D, device=dev, generator=g) * 0.1
     ku = torch.unique(torch.randint(0, U, (U * 100,), device=dev, generator=g) * I +
                       torch.randint(0, I, (U * 100,), device=dev, generator=g))
-    excl = RowSets.from_pairs(ku // I, ku % I, U, I, dev)
+    excl = None if args.no_excl else RowSets.from_pairs(ku // I, ku % I, U, I, dev)
     res = {}
     for mode in args.modes.split(","):
         screen = mode == "screen"
@@ -48,6 +54,15 @@ for D in [int(x) for x in args.dims.split(",")]:
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / args.reps
             res[(mode, sp)] = (v, i)
+            if counts is not None and screen:
+                counts(_buf)
+                names = ["inserted", "hit_group_tiles", "compactions", "escapes", "excl_loads",
+                         "final_entries", "users_finished"]
+                c = [x / (args.reps + 1) for x in _buf[:7]]
+                print("  counts per call: " + ", ".join(f"{n} {v:.4g}" for n, v in zip(names, c)) +
+                      f"  (per user: inserted {c[0] / U:.1f}, compactions {c[2] / U:.2f}, "
+                      f"escapes {c[3] / U:.3f}, excl loads {c[4] / U:.2f}, "
+                      f"final entries {c[5] / max(c[6], 1):.1f})", flush=True)
             print(f"d={D} {mode} splits={sp}: {dt * 1e3:.2f} ms  "
                   f"{U / dt / 1e6:.2f} M users/s  {2 * U * I * D / dt / 1e12:.0f} fp32-equiv TFLOP/s",
                   flush=True)

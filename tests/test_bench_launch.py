@@ -75,3 +75,21 @@ def test_topk_roofline_prices_the_seed_pass_and_the_recorded_exact_share():
     r2 = bench.topk_roofline(nu, I, D, 33, t)
     assert r2["exact_group_tile_share"] is None
     assert abs(r2["achieved"] - base / t / 1e12) < 1e-9 * r2["achieved"]
+
+
+def test_gpus_2_line_carries_the_exchange_exposure():
+    """The N > 1 line's comm block (what the first SCALE run is read by): the all-gathers
+    timed alone (allgather_ms_per_layer, algbw / busbw as nccl-tests define them), and the
+    compute stream's stall on the gathers inside the overlapped forward, per layer
+    (exposed_wait_ms_per_layer; none before layer 0, whose input is replicated) and in all,
+    against the L - 1 layers' isolated gathers (hidden_frac)."""
+    p = _run(["--gpus", "2", "--backend", "gloo", "--launch-check", "--no-cpu-baseline"], _env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    comm = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])["comm"]
+    assert comm["allgather_ms_per_layer"] > 0
+    assert comm["busbw_GBps"] > 0 and abs(comm["busbw_GBps"] - comm["algbw_GBps"] / 2) < 1e-9 * comm["algbw_GBps"]
+    per = comm["exposed_wait_ms_per_layer"]
+    assert len(per) == 3 and per[0] == 0.0 and all(v >= 0 for v in per)
+    assert abs(comm["exposed_wait_ms"] - sum(per)) < 1e-9
+    assert abs(comm["isolated_allgather_ms_per_step"] - 2 * comm["allgather_ms_per_layer"]) < 1e-9
+    assert comm["hidden_frac"] <= 1.0

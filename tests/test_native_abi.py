@@ -78,6 +78,9 @@ def test_argument_validation_without_gpu():
     assert st == 1 and b"32-bit positions" in lib.lg_last_error()
     st = lib.lg_spread_tile_resource_topk_f64(*args, 1000, 2**33, z)
     assert st == 1 and b"32-bit positions" in lib.lg_last_error()
+    # the chunk-bound kernel's per-chunk norm table holds 64 chunks: wider tiles are refused
+    st = lib.lg_score_chunk_bound(one, one, 10, one, one, 64, 0, 4097, one, z, 0, z)
+    assert st == 1 and b"width 4097 > 4096" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
 
