@@ -61,18 +61,24 @@ WORKLOADS = {
     "c4": (200_000, 200_000, 20_000_000, 64, 3),
     "c2": (6_040, 3_706, 800_167, 64, 3),
     "tiny": (20_000, 20_000, 1_000_000, 64, 3),
+    # the power-law secondary input of SURVEY.md §8(d) / BASELINE.md: Zipf(1.1) item
+    # popularity, uniform users (lgcnhs.synth.synth_graph_device(dist="zipf"))
+    "c5-zipf-d64": (1_000_000, 1_000_000, 100_000_000, 64, 3),
+    "c4-zipf": (200_000, 200_000, 20_000_000, 64, 3),
 }
+GRAPH_DIST = {"c5-zipf-d64": "zipf", "c4-zipf": "zipf"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_graph(U, I, E, seed, dev):
-    """Exactly E unique uniform (user, item) pairs on the device; returns the symmetric
-    CSR over U+I nodes (rowptr int64, src int32) plus the sorted interaction keys."""
+def gen_graph(U, I, E, seed, dev, dist="uniform"):
+    """Exactly E unique (user, item) pairs on the device (items uniform or Zipf(1.1)); returns
+    the symmetric CSR over U+I nodes (rowptr int64, src int32) plus the sorted interaction
+    keys."""
     from lgcnhs.synth import synth_graph_device
-    return synth_graph_device(U, I, E, seed, dev)
+    return synth_graph_device(U, I, E, seed, dev, dist=dist)
 
 
 def cpu_threads():
@@ -317,6 +323,66 @@ def time_exchange(prop, shard, D, world, dev, reps=5):
     return {"allgather_ms_per_layer": dt * 1e3, "algbw_GBps": size / dt / 1e9,
             "busbw_GBps": recv / dt / 1e9, "recv_GBps_per_gpu": recv / dt / 1e9,
             "recv_bytes_per_gpu": recv, "pad_ratio": shard.pad_ratio}
+
+
+def bench_other_graph(name, dev, steps, k, topk_users, cpu_parity=True):
+    """A second graph shape at N = 1 (SURVEY.md §8(d)'s power-law input): the propagation
+    (K1 with the long-row pass for hub rows inside the timed forward) with its roofline and
+    PMC traffic, the degree profile that drives it, and the masked top-K on the same graph's
+    exclusion sets (hub items are in most users' histories), its lists checked against the
+    reference op sequence on a CPU sample."""
+    from lgcnhs import _native as NV
+    from lgcnhs.dist import RowShard
+    from lgcnhs.graph import LONG_ROW_THRESHOLD
+    U, I, E, D, L = WORKLOADS[name]
+    N = U + I
+    t0 = time.time()
+    rowptr, src, keys = gen_graph(U, I, E, seed=3, dev=dev, dist=GRAPH_DIST.get(name, "uniform"))
+    nnz = int(src.numel())
+    deg = rowptr[1:] - rowptr[:-1]
+    long_rows = deg > LONG_ROW_THRESHOLD
+    stats = {"dist": GRAPH_DIST.get(name, "uniform"), "zipf_s": 1.1, "users": U, "items": I,
+             "interactions": E, "nnz": nnz, "max_item_degree": int(deg[U:].max()),
+             "max_user_degree": int(deg[:U].max()),
+             "long_rows": int(long_rows.sum()), "long_row_threshold": LONG_ROW_THRESHOLD,
+             "long_row_nnz_share": float(deg[long_rows].sum()) / nnz}
+    dis = torch.empty(N, dtype=torch.float32, device=dev)
+    NV.check(NV.lib().lg_gcn_norm_f32(NV.ptr(rowptr), N, NV.ptr(dis), NV.stream_handle(dev)),
+             "gcn_norm")
+    wgt = torch.empty(nnz, dtype=torch.float32, device=dev)
+    NV.check(NV.lib().lg_gcn_edge_weight_f32(NV.ptr(rowptr), NV.ptr(src), NV.ptr(dis), N, 0,
+                                             NV.ptr(wgt), NV.stream_handle(dev)), "edge weights")
+    shard = RowShard(rowptr, src, N, 0, 1, dev, weight=wgt, chunks=1)
+    del wgt, rowptr, src
+    gen = torch.Generator(device=dev).manual_seed(43)
+    e0 = torch.randn(N, D, device=dev, generator=gen) * 0.1
+    setup = time.time() - t0
+    elapsed, k_s, _ = time_propagation(shard, shard.permute_rows(dis), e0, D, L, steps,
+                                       max(1, steps // 3), 1, dev)
+    alg = nnz * (8 + 4 * D) + N * (4 + 4 * D)
+    traffic, tsrc = load_traffic(name, 1)
+    prop = {"value": nnz * L * steps / elapsed, "unit": "edge-layers/s",
+            "ms_per_step": elapsed / steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": alg / k_s / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": alg / k_s / 1e9 / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": "lg_spmm_layer_f32 + lg_spmm_long_rows_f32 (one layer)",
+                         "avg_launch_ms": k_s * 1e3, "alg_bytes_per_launch": alg}}
+    del shard
+    torch.cuda.empty_cache()
+    out = {"workload": name, "graph": stats, "setup_s": setup, "propagation": prop}
+    try:
+        topk, lists = bench_topk(e0, keys, U, I, D, k, topk_users, 0, 1, dev)
+        if cpu_parity and lists is not None:
+            _, cpu_lists = cpu_baseline_topk(e0, keys, U, I, k, n_users=512)
+            topk["parity_vs_cpu_reference"] = topk_parity(lists[:512], cpu_lists[:512], e0, U,
+                                                          D, k)
+        out["topk"] = topk
+    except Exception as ex:  # a side measurement never hides the main result
+        log(f"{name} topk bench failed: {ex!r}")
+    del e0, keys
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_small_config(dev, k):
@@ -868,6 +934,9 @@ def main():
     ap.add_argument("--layout", default="bipartite", choices=["bipartite", "rows"],
                     help="N>1 row sharding: users and items sharded separately with "
                          "cross-layer overlap (bipartite) or contiguous node rows (rows)")
+    ap.add_argument("--other-graphs", nargs="*", default=["c5-zipf-d64"],
+                    help="N = 1: also measure these graph shapes (other_graphs; the Zipf(1.1) "
+                         "power-law input of SURVEY.md §8(d))")
     ap.add_argument("--launch-check", action="store_true",
                     help="rank plumbing only (process group + one all-reduce), no GPU work")
     args = ap.parse_args()
@@ -906,7 +975,8 @@ def main():
     U, I, E, D, L = WORKLOADS[args.workload]
     N = U + I
     t0 = time.time()
-    rowptr, src, keys = gen_graph(U, I, E, seed=0, dev=dev)
+    rowptr, src, keys = gen_graph(U, I, E, seed=0, dev=dev,
+                                  dist=GRAPH_DIST.get(args.workload, "uniform"))
     nnz = int(src.numel())
     from lgcnhs import _native as NV
     dis = torch.empty(N, dtype=torch.float32, device=dev)
@@ -986,6 +1056,17 @@ def main():
         del e2
         torch.cuda.empty_cache()
 
+    other_graphs = {}
+    if world == 1:
+        for name in args.other_graphs:
+            try:
+                other_graphs[name.split("-d")[0].replace("c5-", "").replace("c4-", "c4_")] = \
+                    bench_other_graph(name, dev, max(3, args.steps // 2), args.k,
+                                      args.topk_users, cpu_parity=not args.no_cpu_baseline)
+            except Exception as ex:  # a side measurement never hides the main result
+                log(f"{name} bench failed: {ex!r}")
+            torch.cuda.empty_cache()
+
     train = None
     if train_graph is not None:  # after the timed forwards: it leaves the caches cold
         try:
@@ -1055,6 +1136,7 @@ def main():
             "spread": spread,
             "train": train,
             "other_dims": extra,
+            "other_graphs": other_graphs,
             "c2_ml1m_shape": small,
             "cpu_baseline": cpu,
             "cpu_baseline_topk": cpu_topk,

@@ -156,7 +156,9 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
  *   umarg[u] >= (||du|| I + (||eu[u]|| + ||du||) DI + (2.01 dim 2^-24 + 2^-22) ||eu[u]|| I)
  * with du = eu[u] - bf16(eu[u]), I = max_i ||ei[i]||, DI = max_i ||ei[i] - bf16(ei[i])||
  * (lgcnhs.ops.screen_margins, from lg_bound_prep_f32's norm_up / err_up; the round-3 form
- * 0.0081 ||eu[u]|| I is larger and also valid). k <= 32: one pass keeps per user the items
+ * 0.0081 ||eu[u]|| I is larger and also valid). Every umarg[u] must be finite (so every
+ * embedding is finite and no product overflows): lgcnhs.ops routes other inputs to
+ * lg_score_topk_f32. k <= 32: one pass keeps per user the items
  * whose bound can still reach the k-th largest lower bound, and ranks those by the exact chain
  * at the end; k > 32: a tile whose bound beats a user's threshold is recomputed exactly.
  * Workspace and splits as lg_score_topk_f32. For k <= 32 on catalogs of >= 1024 k items a

@@ -627,10 +627,35 @@ __device__ __forceinline__ float ubound(float b, float m) {
 constexpr uint32_t kFinal = 0x80000000u;  // list entry id bit: the key is the final value
 
 #ifdef LG_TOPK_COUNT  // measurement builds only: event counts of k_topk_ring (lg_topk_counts)
-__device__ unsigned long long g_topk_counts[8];
+__device__ unsigned long long g_topk_counts[16];
 #define LG_COUNT(i, v) (cnt_ev[i] += (v))
+// cycles of a phase: LG_CLK0(t) before it, LG_CLK1(i, t) after it (slot i)
+#define LG_CLK0(t) const unsigned long long t = clock64()
+#define LG_CLK1(i, t) (cnt_ev[i] += clock64() - (t))
 #else
 #define LG_COUNT(i, v) ((void)0)
+#define LG_CLK0(t) ((void)0)
+#define LG_CLK1(i, t) ((void)0)
+#endif
+
+// the k <= 32 ring kernel's shape: list capacity, fragment-ring buffers, chunks a wave issues
+// ahead, chunks between a piece's issue and its arrival signal (measurement builds may
+// override them: -DLG_RING_CAP=... etc.)
+#ifndef LG_RING_CAP
+#define LG_RING_CAP 56
+#endif
+#ifndef LG_RING_NBUF
+#define LG_RING_NBUF 5
+#endif
+#ifndef LG_RING_LA
+#define LG_RING_LA 3
+#endif
+#ifndef LG_RING_LAG
+#define LG_RING_LAG 1
+#endif
+// user groups per wave (2: 8 waves, two per SIMD; 4: 4 waves, one per SIMD)
+#ifndef LG_RING_NG
+#define LG_RING_NG 2
 #endif
 
 template <int D, int NG, int WAVES, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
@@ -642,12 +667,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
     float *__restrict__ part_val, int32_t *__restrict__ part_idx,
     const float *__restrict__ seed_val) {
+  // WAVES waves x NG groups of 16 users (the MFMA columns): 256 users per CU
+  static_assert(NG * WAVES * 16 == 256, "256 users per block");
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
   static_assert(CAP <= 64 && CAP >= 48, "one list entry per lane, room for k + a tile");
-  // the fragment ring: chunks of CI items (8 KiB, one 16-byte LDS-DMA piece per thread)
-  constexpr int CI = 512 * WAVES / D, TPC = CI / 16, PR = D / 8, RB = 2 * D;
-  static_assert(CI * PR == 64 * WAVES, "one DMA piece per thread and chunk");
+  // the fragment ring: chunks of CI items (CB bytes, PPT 16-byte LDS-DMA pieces per thread)
+  constexpr int CB = D >= 64 || WAVES >= 8 ? 8192 : 4096;  // (>= one 16-byte piece per thread)
+  constexpr int CI = CB / (2 * D), TPC = CI / 16, PR = D / 8, RB = 2 * D;
+  constexpr int PPT = CB / 16 / (64 * WAVES);
+  static_assert(PPT >= 1 && CI * PR == 64 * WAVES * PPT, "whole DMA pieces per thread");
   static_assert(LAG >= 1 && LA > LAG && NBUF > LA, "ring shape");
   // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane)
   constexpr int TPC_S = TPC < 4 ? TPC : 4;
@@ -657,7 +686,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   __shared__ uint32_t li[WAVES][NG][16][SEEDP ? 1 : CAP];
   __shared__ int exs[WAVES][64];  // exclusion runs; the exact chain's results
   __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
-  __shared__ uint32_t arrive[NBUF], done[NBUF];
+  __shared__ uint32_t prog[WAVES];  // the fragment ring's progress words (below)
 
   const int wave = threadIdx.x / 64;
   const int lane = lane_id();
@@ -713,8 +742,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   }
 #ifdef LG_TOPK_COUNT
   // 0 inserted entries, 1 group-tiles with a hit, 2 compactions, 3 escapes (lists made exact
-  // mid-stream), 4 exclusion-row loads, 5 entries ranked exactly at the end, 6 users finished
-  unsigned long long cnt_ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // mid-stream), 4 exclusion-row loads, 5 entries ranked exactly at the end, 6 users finished;
+  // cycles (clock64) in 8 ring waits, 9 screen + tests, 10 insertion, 11 compaction, 12 the
+  // final ranking, 13 the whole wave
+  unsigned long long cnt_ev[16] = {};
+  LG_CLK0(t_all);
 #endif
   const uint64_t same_user = 0x0001000100010001ull << ul;
   // retire the prologue loads with a wait hipcc sees (vmcnt(0)): otherwise its waitcnt pass
@@ -728,6 +760,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   // bit. Results pass through exs (lane e reads its own).
   auto exact_entries = [&](int64_t user, uint64_t want, int item) __attribute__((always_inline)) {
     float uf[Q];
+    user = user < n_users ? user : n_users - 1;  // (callers pass valid users; a clamp is cheap)
     load_piece<Q>(eu + user * D + gq * Q, uf);
     constexpr int NB = CAP / 16 + (CAP % 16 ? 1 : 0);  // 16-entry batches
     constexpr int BL = D <= 64 ? 4 : 2;               // batches whose rows load together
@@ -738,7 +771,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       for (int b = 0; b < BL; ++b) {
         const int e = 16 * (b0 + b) + ul;
         const int it = __shfl(item, e < 64 ? e : 63);
-        const bool w = b0 + b < NB && e < 64 && ((want >> e) & 1ull);
+        const bool w = b0 + b < NB && e < 64 && ((want >> e) & 1ull) && it >= 0 &&
+                       it < n_items;
         load_piece<Q>(ei + (int64_t)(w ? it : 0) * D + gq * Q, af[b]);
       }
 #pragma unroll
@@ -770,13 +804,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   // best k kept, all final. Returns, on lane e < k, the e-th output entry when fin.
   // (g is a run-time, wave-uniform group index: the loop has one compaction site, not one
   // per group and tile -- inlined copies made the kernel ~54 KB of code)
-  auto gget = [&](const auto (&a)[NG], int g) __attribute__((always_inline)) {
-    auto v = a[0];
-#pragma unroll
-    for (int j = 1; j < NG; ++j)
-      if (g == j) v = a[j];
-    return v;
-  };
+  // (an explicit conditional chain: a helper taking the array by reference kept the per-group
+  // arrays in scratch memory -- private segment 128 B/lane -- instead of registers)
+  static_assert(NG == 2 || NG == 4, "gget's chains");
+#define gget(a, g)                                                                              \
+  (NG == 2 ? ((g) ? (a)[1 % NG] : (a)[0])                                                       \
+           : ((g) == 0 ? (a)[0] : (g) == 1 ? (a)[1 % NG] : (g) == 2 ? (a)[2 % NG] : (a)[3 % NG]))
   auto compact_user = [&](int g, int u, int lim, bool fin, float &ov, int &oi)
       __attribute__((always_inline)) {
     const int n = __shfl(gget(cnt, g), u);
@@ -873,18 +906,27 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       }
   };
   // compact every list that could overflow on the next tile (+16 entries max per tile)
-  auto compact_over = [&](int lim) __attribute__((always_inline)) {
-    uint32_t need = 0;  // bit 16 g + u
+  // the lists holding more than `over` entries (bit 16 g + u)
+  static_assert(NG <= 4, "16 NG list bits");
+  auto lists_over = [&](int over) __attribute__((always_inline)) {
+    uint64_t need = 0;
 #pragma unroll
     for (int g = 0; g < NG; ++g)
-      need |= (uint32_t)(__ballot(cnt[g] > CAP - 16) & 0xffffull) << (16 * g);
+      need |= (__ballot(cnt[g] > over) & 0xffffull) << (16 * g);
+    return need;
+  };
+  auto compact_one = [&](int b, int lim) __attribute__((always_inline)) {
+    float ov;
+    int oi;
+    compact_user(b >> 4, b & 15, lim, false, ov, oi);
+  };
+  auto compact_over = [&](int lim) __attribute__((always_inline)) {
+    uint64_t need = lists_over(CAP - 16);
     wave_sync();
     while (need) {
-      const int b = __builtin_ctz(need);
+      const int b = __builtin_ctzll(need);
       need &= need - 1;
-      float ov;
-      int oi;
-      compact_user(b >> 4, b & 15, lim, false, ov, oi);
+      compact_one(b, lim);
     }
   };
   // insertion of group g's bf16 products accb of tile t (lane (ul, gq): items 4 gq + r of the
@@ -894,7 +936,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const bool cand = rel + r < n_valid && above(acc[r] + marg[g], thr[g]);
+      // (the margins are finite -- the caller's contract -- so a bound compares as a number:
+      // padding users past n_users, thr = +inf, never enter)
+      const bool cand = rel + r < n_valid && acc[r] + marg[g] > thr[g];
       const uint64_t bal = __ballot(cand);
       LG_COUNT(0, __popcll(bal));
       if (bal) {
@@ -918,79 +962,74 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       cmax[g][tt] = f32x4{neg_inf<float>(), neg_inf<float>(), neg_inf<float>(),
                           neg_inf<float>()};
   {
-    // The block's waves share the bf16 item fragments through LDS: chunks of CI items (8 KiB,
-    // one 16-byte LDS-DMA piece per thread: global_load_lds_dwordx4, no VGPRs) in a ring of
-    // NBUF buffers; the 16-byte pieces of row r stored XOR-swizzled by sw(r) through the
-    // SOURCE address, so the fragment reads of any 16 consecutive lanes hit distinct banks
+    // The block's waves share the bf16 item fragments through LDS: chunks of CI items (CB
+    // bytes, PPT 16-byte LDS-DMA pieces per thread: global_load_lds_dwordx4, no VGPRs) in a
+    // ring of NBUF buffers; the 16-byte pieces of row r stored XOR-swizzled by sw(r) through
+    // the SOURCE address, so the fragment reads of any 16 consecutive lanes hit distinct banks
     // (the layout of csrc/gbound.hip).
-    // No block barrier per chunk: the waves drift apart, coupled by two LDS counters per
-    // buffer:
-    //   arrive[b]: +1 per wave once its piece of the chunk in b has landed (its own vmcnt);
-    //   done[b]:   +1 per wave once it has read the chunk in b.
-    // Wave w at chunk c: (1) once every wave is done with chunk c + LA - NBUF, issue its piece
-    // of chunk c + LA into that buffer; (2) vmcnt(LAG) -- its pieces up to chunk c + LA - LAG
-    // have landed -- and signal arrival for chunk c + LA - LAG; (3) wait until all WAVES
-    // pieces of chunk c have arrived; (4) screen it; (5) signal done. The slowest wave never
-    // waits (the others are past the chunks it needs them for), so the ring cannot deadlock; a
-    // wave is at most min(LA - LAG, NBUF - LA) chunks ahead of the slowest. The DMA is inline
-    // asm with no register outputs, invisible to hipcc's waits (hipcc's own
-    // __builtin_amdgcn_global_load_lds puts vmcnt(0) before every LDS read, as it cannot tell
-    // the ring's buffers apart); an untracked load only makes hipcc's own vmcnt waits stricter
-    // (the counter retires in order).
+    // No block barrier: the waves drift apart, coupled only through one progress word per wave
+    // in LDS, prog[w] = consumed << 16 | landed (16-bit counts, compared with wrap-around: the
+    // drift is < NBUF):
+    //   landed:   chunks whose pieces from wave w have landed in LDS (its own vmcnt);
+    //   consumed: chunks wave w has read into registers.
+    // Wave w at chunk c: (1) once every wave has consumed chunk c + LA - NBUF, issue its pieces
+    // of chunk c + LA into that chunk's buffer; (2) vmcnt: its pieces up to chunk c + LA - LAG
+    // have landed; (3) once every wave's pieces of chunk c + 1 have landed, read that chunk
+    // (software pipeline, below) and publish both counts. Each wave writes only its own word (a
+    // plain LDS store from lane 0, no atomics) and checks all WAVES words with one lane-parallel
+    // LDS read (lane j reads wave j's word), issued right after its publication so that its
+    // latency hides behind the chunk's MFMAs; only a failed check spins (and re-reads). The LDS
+    // serves each wave's operations in order, so a wave's fragment reads have been performed
+    // before any wave can see its consumed count (and DMA into that buffer), and a DMA piece has
+    // landed before the landed count that covers it is published. The slowest wave never
+    // waits, so the ring cannot deadlock. The DMA is inline asm with no register outputs,
+    // invisible to hipcc's waits (hipcc's own __builtin_amdgcn_global_load_lds puts vmcnt(0)
+    // before every LDS read, as it cannot tell the ring's buffers apart); an untracked load
+    // only makes hipcc's own vmcnt waits stricter (the counter retires in order).
     auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
-    const int pp = (int)threadIdx.x, pr = pp / PR;
-    const int pcol = 8 * ((pp % PR) ^ sw(pr));
     auto dma = [&](int c) __attribute__((always_inline)) {
-      int64_t it = i0 + (int64_t)c * CI + pr;
-      it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
-      const __bf16 *src = eib + it * D + pcol;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(
-          __attribute__((address_space(3))) char *)(frs[c % NBUF] + 1024 * wave));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) {
+        const int p = 64 * WAVES * j + (int)threadIdx.x, r = p / PR;
+        int64_t it = i0 + (int64_t)c * CI + r;
+        it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
+        const __bf16 *src = eib + it * D + 8 * ((p % PR) ^ sw(r));
+        const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(
+            __attribute__((address_space(3))) char *)(frs[c % NBUF] + 1024 * (WAVES * j + wave)));
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+      }
     };
-    // the counters are monotone: chunk c is the (c / NBUF + 1)-th generation of buffer c % NBUF
-    auto signal = [&](uint32_t *ctr) __attribute__((always_inline)) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wave's reads are complete)
-      if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t landed = 0u, consumed = 0u;  // this wave's counts (wave-uniform)
+    uint32_t pv_ = 0u;  // the last read of every wave's progress word (lane j: wave j)
+    auto publish = [&]() __attribute__((always_inline)) {
+      asm volatile("" ::: "memory");  // (after the reads / the vmcnt wait before it)
+      if (lane == 0)
+        __hip_atomic_store(&prog[wave], (consumed << 16) | (landed & 0xffffu), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    auto wait_for = [&](uint32_t *ctr, uint32_t target) __attribute__((always_inline)) {
-      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    auto read_prog = [&]() __attribute__((always_inline)) {
+      return __hip_atomic_load(&prog[lane < WAVES ? lane : 0], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    // every wave's count (bits `sh`) has reached `need` (16-bit wrap-around)
+    auto all_reached = [&](uint32_t v, uint32_t need, int sh) __attribute__((always_inline)) {
+      const int16_t d = (int16_t)(uint16_t)(((v >> sh) - need) & 0xffffu);
+      return __ballot(lane < WAVES && d < 0) == 0;
+    };
+    auto wait_reached = [&](uint32_t &v, uint32_t need, int sh) __attribute__((always_inline)) {
+      while (!all_reached(v, need, sh)) {
         __builtin_amdgcn_s_sleep(1);
+        v = read_prog();
+      }
       asm volatile("" ::: "memory");
     };
-    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform)
-    if (threadIdx.x < NBUF) {
-      arrive[threadIdx.x] = 0u;
-      done[threadIdx.x] = 0u;
-    }
-    __syncthreads();  // (the only block barrier)
-    for (int c = 0; c < LA; ++c) dma(c);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG) : "memory");
-    for (int c = 0; c < LA - LAG; ++c) signal(&arrive[c]);
-    for (int c = 0; c < n_c; ++c) {
-#ifndef LG_RING_PROBE_NORING  // (measurement builds: no ring protocol, chunk 0's buffer reread)
-      {
-        const int cn = c + LA, cp = cn - NBUF;  // chunk cn replaces chunk cp in its buffer
-        if (cp >= 0) wait_for(&done[cp % NBUF], (uint32_t)(WAVES * (cp / NBUF + 1)));
-        dma(cn);  // (chunks past the split: harmless clamped reads, signalled like the rest)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG) : "memory");
-        signal(&arrive[(cn - LAG) % NBUF]);
-      }
-      wait_for(&arrive[c % NBUF], (uint32_t)(WAVES * (c / NBUF + 1)));
+    typedef bf16x8 Frags[TPC][S];
+    typedef f32x4 Accs[TPC][NG];
+    auto read_chunk = [&](int c, Frags &fr) __attribute__((always_inline)) {
       const char *fb = frs[c % NBUF];
-#else
-      const char *fb = frs[0];
-#endif
-      const int t0 = c * TPC;
-      // The chunk's TPC tiles are screened together -- every fragment read, then every bf16
-      // MFMA, then the hit tests -- so the reads and the MFMA chains of different tiles
-      // overlap instead of one tile's LDS -> MFMA -> compare chain at a time. The tests use
-      // the thresholds of the chunk start: never above the running ones (they only rise), so
-      // a tile they rule out holds no item that could enter later either.
-      bf16x8 fr[TPC][S];
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt) {
         const int r = 16 * tt + ul;
@@ -999,60 +1038,72 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
           fr[tt][s] =
               *reinterpret_cast<const bf16x8 *>(fb + r * RB + 16 * ((4 * s + gq) ^ sw(r)));
       }
-      f32x4 accb[TPC][NG];
+    };
+    auto mfma_chunk = [&](const Frags &fr, Accs &acc) __attribute__((always_inline)) {
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt)
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-          accb[tt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[tt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < S; ++s)
-            accb[tt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[tt][s], ub[g][s],
-                                                                  accb[tt][g], 0, 0, 0);
+            acc[tt][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[tt][s], ub[g][s],
+                                                                acc[tt][g], 0, 0, 0);
         }
-#ifndef LG_RING_PROBE_NORING
-      signal(&done[c % NBUF]);  // (the fragments are in registers: the buffer is free)
-#endif
-      if constexpr (SEEDP) {
-        // the seed pass: each lane's running maxima of the lower bounds (past the range: -inf;
-        // a NaN stays NaN and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
+    };
+    // The chunk's test: per group the largest product of the chunk plus the margin against
+    // the threshold, one ballot per group; returns the groups (bits) with a possible entrant.
+    // Tests run against the thresholds of that moment: never above the later ones (they only
+    // rise). (Finite margins and embeddings, the caller's contract: a bound is a number; a
+    // NaN product -- never an exact score that enters -- would not hit.)
+    auto test_chunk = [&](const Accs &acc) __attribute__((always_inline)) {
+      uint32_t gm = 0;
 #pragma unroll
-        for (int tt = 0; tt < TPC; ++tt) {
-          const int rel = (t0 + tt) * 16 + gq * 4;
+      for (int g = 0; g < NG; ++g) {
+        float m = max4(acc[0][g]);
 #pragma unroll
-          for (int g = 0; g < NG; ++g)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float lb = rel + r < n_valid ? lbound(accb[tt][g][r], marg[g])
-                                                 : neg_inf<float>();
-              cmax[g][tt % TPC_S][r] = __builtin_elementwise_maximum(cmax[g][tt % TPC_S][r], lb);
-            }
-        }
-        continue;
+        for (int tt = 1; tt < TPC; ++tt)
+          m = __builtin_elementwise_maximum(
+              m, __builtin_elementwise_maximum(
+                     __builtin_elementwise_maximum(acc[tt][g][0], acc[tt][g][1]),
+                     __builtin_elementwise_maximum(acc[tt][g][2], acc[tt][g][3])));
+        if (__ballot(m + marg[g] > thr[g]) != 0) gm |= 1u << g;
       }
+      return gm;
+    };
+    // the seed pass: each lane's running maxima of the lower bounds (past the range: -inf; a
+    // NaN stays NaN and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
+    auto seed_chunk = [&](int c, const Accs &acc) __attribute__((always_inline)) {
+      const int t0 = c * TPC;
+#pragma unroll
+      for (int tt = 0; tt < TPC; ++tt) {
+        const int rel = (t0 + tt) * 16 + gq * 4;
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float lb = rel + r < n_valid ? lbound(acc[tt][g][r], marg[g])
+                                               : neg_inf<float>();
+            cmax[g][tt % TPC_S][r] = __builtin_elementwise_maximum(cmax[g][tt % TPC_S][r], lb);
+          }
+      }
+    };
+    // chunk c's hit tiles (after its chunk test hit the groups gm): per-tile tests of those
+    // groups, then the insertions in tile order; when a list could overflow on the next tile,
+    // the lists are compacted (one code site) and the insertion resumes after that tile. The
+    // products and the tile index pass an opaque (empty) asm inside each tile's insertion:
+    // otherwise hipcc hoists the insertions' set-up -- bound sums, item ids, range tests, SGPR
+    // spills -- out of the tile loop to the top of this path (~100 instructions per hit chunk).
+    auto process_hits = [&](int c, const Accs &acc, uint32_t gm) __attribute__((always_inline)) {
+      const int t0 = c * TPC;
       uint32_t hits = 0;  // bit tt * NG + g: group g's screen hit in tile tt (wave-uniform)
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt)
 #pragma unroll
         for (int g = 0; g < NG; ++g)
-          // (a NaN bound, e.g. from a non-finite embedding or margin, enters)
-          if (__ballot(above(max4(accb[tt][g]) + marg[g], thr[g])) != 0)
+          if (((gm >> g) & 1u) && __ballot(max4(acc[tt][g]) + marg[g] > thr[g]) != 0)
             hits |= 1u << (tt * NG + g);
       if (t0 + TPC > n_t) hits &= (1u << ((n_t - t0) * NG)) - 1u;  // (tiles past the split)
-#ifdef LG_SCREEN_PROBE  // measurement builds only (wrong lists): the screen and its tests alone
-      asm volatile("" ::"s"(hits));
-      hits = 0u;
-#endif
-      if (hits == 0) continue;  // (the common case: one branch)
-      // The hit tiles in order; when a list could overflow on the next tile, the lists are
-      // compacted (one code site) and the insertion resumes after that tile. The bf16
-      // products pass an opaque (empty) asm first: otherwise hipcc hoists the insertion's
-      // set-up -- 32 bound sums, item ids, range tests, SGPR spills -- out of this rare path
-      // into every chunk (~150 VALU per chunk measured).
-#pragma unroll
-      for (int tt = 0; tt < TPC; ++tt)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) asm volatile("" : "+v"(accb[tt][g]));
       int tt0 = 0;
       while (hits) {
         int stop = TPC;
@@ -1061,9 +1112,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
           const uint32_t th = (hits >> (tt * NG)) & ((1u << NG) - 1u);
           if (tt < tt0 || stop != TPC || th == 0) continue;  // (wave-uniform)
           LG_COUNT(1, __popc(th));
+          LG_CLK0(t_ins);
+          int t = t0 + tt;
+          asm volatile("" : "+s"(t));
 #pragma unroll
           for (int g = 0; g < NG; ++g)
-            if ((th >> g) & 1u) insert_bound(t0 + tt, g, accb[tt][g]);
+            if ((th >> g) & 1u) {
+              f32x4 a = acc[tt][g];
+              asm volatile("" : "+v"(a));
+              insert_bound(t, g, a);
+            }
+          LG_CLK1(10, t_ins);
           bool over = false;
 #pragma unroll
           for (int g = 0; g < NG; ++g) over |= cnt[g] > CAP - 16;
@@ -1071,10 +1130,62 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         }
         if (stop == TPC) break;
         const int l = (int)i0 + (t0 + stop + 1) * 16;
+        LG_CLK0(t_cmp);
         compact_over(l < lim_end ? l : lim_end);
+        LG_CLK1(11, t_cmp);
         tt0 = stop + 1;
         hits &= ~((1u << (tt0 * NG)) - 1u);
       }
+    };
+    const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform)
+    if (threadIdx.x < WAVES) prog[threadIdx.x] = 0u;
+    __syncthreads();  // (the only block barrier)
+    for (int c = 0; c < LA; ++c) dma(c);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG * PPT) : "memory");
+    landed = LA - LAG;
+    publish();
+    pv_ = read_prog();
+    for (int c = 0; c < n_c; ++c) {
+      LG_CLK0(t_ring);
+      {
+        const int cn = c + LA, cp = cn - NBUF;  // chunk cn replaces chunk cp in its buffer
+        if (cp >= 0) wait_reached(pv_, (uint32_t)(cp + 1), 16);
+        LG_CLK1(14, t_ring);
+        LG_CLK0(t_dma);
+        dma(cn);  // (chunks past the split: harmless clamped reads, published like the rest)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG * PPT) : "memory");
+        landed = (uint32_t)(cn - LAG + 1);
+        LG_CLK1(15, t_dma);
+      }
+      LG_CLK0(t_arr);
+      wait_reached(pv_, (uint32_t)(c + 1), 0);
+      LG_CLK1(7, t_arr);
+      LG_CLK1(8, t_ring);
+      LG_CLK0(t_scr);
+      // The chunk's TPC tiles are screened together -- every fragment read, then every bf16
+      // MFMA, then the test -- so the reads and the MFMA chains of different tiles overlap
+      // instead of one tile's LDS -> MFMA -> compare chain at a time.
+      Frags fr;
+      Accs acc;
+      read_chunk(c, fr);
+      mfma_chunk(fr, acc);
+      // (the fragments are in registers: the buffer is free) -- published with this chunk's
+      // landed count, and the next check's read issued right away
+      consumed = (uint32_t)(c + 1);
+      publish();
+      pv_ = read_prog();
+      if constexpr (SEEDP) {
+        seed_chunk(c, acc);
+        LG_CLK1(9, t_scr);
+        continue;
+      }
+      uint32_t gm = test_chunk(acc);
+      LG_CLK1(9, t_scr);
+#ifdef LG_SCREEN_PROBE  // measurement builds only (wrong lists): the screen and its tests alone
+      asm volatile("" ::"s"(gm));
+      gm = 0;
+#endif
+      if (gm != 0) process_hits(c, acc, gm);  // (rare: one branch otherwise)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA in flight at the exit)
   }
@@ -1122,6 +1233,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     }
     return;
   }
+  LG_CLK0(t_fin);
 #pragma unroll 1
   for (int b = 0; b < 16 * NG; ++b) {  // (user ubase + b = group b / 16, column b % 16)
     {
@@ -1143,12 +1255,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     }
   }
 #ifdef LG_TOPK_COUNT
+  LG_CLK1(12, t_fin);
+  LG_CLK1(13, t_all);
   if (lane == 0)
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 16; ++i)
       if (cnt_ev[i]) __hip_atomic_fetch_add(&g_topk_counts[i], cnt_ev[i], __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
+
+#undef gget
 
 // Merge n_splits partial lists (each sorted, item ranges ascending by split) per user.
 template <int M>
@@ -1334,22 +1450,6 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
   out_val[u * k + k - 1] = m;
 }
 
-// the k <= 32 ring kernel's shape: list capacity, fragment-ring buffers, chunks a wave issues
-// ahead, chunks between a piece's issue and its arrival signal (measurement builds may
-// override them: -DLG_RING_CAP=... etc.)
-#ifndef LG_RING_CAP
-#define LG_RING_CAP 56
-#endif
-#ifndef LG_RING_NBUF
-#define LG_RING_NBUF 5
-#endif
-#ifndef LG_RING_LA
-#define LG_RING_LA 3
-#endif
-#ifndef LG_RING_LAG
-#define LG_RING_LAG 1
-#endif
-
 template <int D>
 static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float *ei,
                                  const __bf16 *eub, const __bf16 *eib, const float *umarg,
@@ -1367,13 +1467,14 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx);                 \
   }
-  // k <= 32: one 8-wave block per CU (RING_CAP-entry lists for 256 users + the fragment
-  // ring) shares the item fragments; larger lists keep 2-wave blocks that load their own
+  // k <= 32: one block per CU (RING_CAP-entry lists for 256 users + the fragment ring)
+  // shares the item fragments; larger lists keep 2-wave blocks that load their own
 #define LG_RING_LAUNCH(SEEDP)                                                                 \
   {                                                                                           \
     const int64_t tiles = (n_users + 255) / 256;                                              \
-    k_topk_ring<D, 2, 8, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, LG_RING_LAG, SEEDP>           \
-        <<<dim3((unsigned)(tiles * n_splits)), dim3(512), 0, stream>>>(                       \
+    k_topk_ring<D, LG_RING_NG, 16 / LG_RING_NG, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,         \
+                LG_RING_LAG, SEEDP>                                                           \
+        <<<dim3((unsigned)(tiles * n_splits)), dim3(1024 / LG_RING_NG), 0, stream>>>(         \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
@@ -1552,12 +1653,12 @@ extern "C" int lg_score_dense_f32(const float *eu, const float *ei, int64_t n_us
 }
 
 #ifdef LG_TOPK_COUNT
-// measurement builds only: read and clear k_topk_ring's event counts (8 x uint64, host)
-extern "C" int lg_topk_counts(unsigned long long *host8) {
+// measurement builds only: read and clear k_topk_ring's event counts (16 x uint64, host)
+extern "C" int lg_topk_counts(unsigned long long *host16) {
   if (hipDeviceSynchronize() != hipSuccess) return LG_ERR_HIP;
-  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_topk_counts), 64) != hipSuccess) return LG_ERR_HIP;
-  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_topk_counts), z, 64) != hipSuccess) return LG_ERR_HIP;
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_topk_counts), 128) != hipSuccess) return LG_ERR_HIP;
+  const unsigned long long z[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_topk_counts), z, 128) != hipSuccess) return LG_ERR_HIP;
   return LG_OK;
 }
 #endif

@@ -264,9 +264,12 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     if screen and nu > 0:
         ub, un, ue = bound_operands(eu, with_err=True)
         ib, inorm, ierr = bound_operands(ei, with_err=True)
-        # (a non-finite embedding makes a margin NaN or inf: the kernel then keeps every item
-        # of those users and ranks them exactly, so the lists stay lg_score_topk_f32's)
         umarg = screen_margins(un, ue, inorm, ierr, d)
+        if not bool(torch.isfinite(umarg).all()):
+            # a non-finite (or overflowing) embedding makes the margins non-finite: the screen's
+            # bounds are then no numbers, and the plain kernel (the same lists by definition)
+            # ranks every item -- lg_score_topk_screened_f32's contract (include/lgcnhs.h)
+            return score_topk(eu, ei, k, excl, mask_value, n_splits, screen=False)
         N.check(N.lib().lg_score_topk_screened_f32(
             N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d, ex_rp, ex_c,
             float(mask_value), int(k), ns, N.ptr(val), N.ptr(idx), N.ptr(ws), ws_bytes,

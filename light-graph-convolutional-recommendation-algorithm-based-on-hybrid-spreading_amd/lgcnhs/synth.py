@@ -61,23 +61,48 @@ def synth_interactions(n_users: int, n_items: int, n_edges: int, seed: int = 0,
     return keys // I, keys % I
 
 
-def synth_graph_device(n_users: int, n_items: int, n_edges: int, seed: int, device):
-    """Exactly n_edges unique uniform (user, item) pairs drawn on the device (the C4/C5
-    scale, where numpy's unique over 10^8 keys is too slow). Returns the symmetric CSR over
-    U+I nodes (rowptr int64, src int32; users then items, each row ascending) and the sorted
-    interaction keys user * I + item (int64)."""
+def synth_graph_device(n_users: int, n_items: int, n_edges: int, seed: int, device,
+                       dist: str = "uniform", zipf_s: float = 1.1):
+    """Exactly n_edges unique (user, item) pairs drawn on the device (the C4/C5 scale, where
+    numpy's unique over 10^8 keys is too slow): users uniform; items uniform, or with
+    ``dist="zipf"`` Zipf(zipf_s) popularity (rank r drawn with weight r^-s by inverse-CDF
+    sampling; ranks mapped to a seeded random permutation of the item ids, so the hubs are
+    spread over the id range as in real catalogs). A popular item saturates at n_users
+    interactions (pairs are unique), so the draws are topped up until E pairs exist.
+    Returns the symmetric CSR over U+I nodes (rowptr int64, src int32; users then items, each
+    row ascending) and the sorted interaction keys user * I + item (int64)."""
     import torch
 
     from .graph import _rowptr_from_sorted
     U, I, E = int(n_users), int(n_items), int(n_edges)
+    if E > U * I:
+        raise ValueError(f"E={E} > U*I")
     g = torch.Generator(device=device).manual_seed(seed)
+    if dist == "zipf":
+        cdf = torch.cumsum(torch.arange(1, I + 1, dtype=torch.float64, device=device)
+                           .pow(-float(zipf_s)), 0)
+        cdf /= cdf[-1].clone()
+        perm = torch.randperm(I, device=device, generator=g)
+
+        def draw_items(n):
+            r = torch.searchsorted(cdf, torch.rand(n, dtype=torch.float64, device=device,
+                                                   generator=g))
+            return perm[r.clamp_(max=I - 1)]
+    elif dist == "uniform":
+        def draw_items(n):
+            return torch.randint(0, I, (n,), device=device, generator=g)
+    else:
+        raise ValueError(f"unknown dist {dist!r}")
     keys = torch.empty(0, dtype=torch.int64, device=device)
+    over = 1.02  # draws per missing pair, re-estimated from each round's yield
     while keys.numel() < E:
-        n = int((E - keys.numel()) * 1.02) + 1024
+        have = keys.numel()
+        n = int((E - have) * over) + 1024
         u = torch.randint(0, U, (n,), device=device, generator=g)
-        i = torch.randint(0, I, (n,), device=device, generator=g)
-        keys = torch.unique(torch.cat([keys, u * I + i]))
-        del u, i
+        keys = torch.unique(torch.cat([keys, u * I + draw_items(n)]))
+        del u
+        gained = keys.numel() - have
+        over = min(8.0, max(1.02, 1.05 * n / max(gained, 1)))
     if keys.numel() > E:
         pick = torch.randperm(keys.numel(), device=device, generator=g)[:E]
         keys = torch.sort(keys[pick]).values

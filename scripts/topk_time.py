@@ -29,7 +29,7 @@ _lib = NV.lib()
 counts = getattr(_lib, "lg_topk_counts", None)  # (measurement builds with -DLG_TOPK_COUNT)
 if counts is not None:
     counts.argtypes, counts.restype = [ctypes.c_void_p], ctypes.c_int
-    _buf = (ctypes.c_ulonglong * 8)()
+    _buf = (ctypes.c_ulonglong * 16)()
     counts(_buf)
 
 dev = torch.device("cuda:0")
@@ -63,6 +63,13 @@ for D in [int(x) for x in args.dims.split(",")]:
                       f"  (per user: inserted {c[0] / U:.1f}, compactions {c[2] / U:.2f}, "
                       f"escapes {c[3] / U:.3f}, excl loads {c[4] / U:.2f}, "
                       f"final entries {c[5] / max(c[6], 1):.1f})", flush=True)
+                cyc = [x / (args.reps + 1) for x in _buf[:16]]
+                if cyc[13]:
+                    print("  cycles (share of the wave's): " + ", ".join(
+                        f"{n} {cyc[i] / cyc[13]:.3f}" for n, i in (
+                            ("ring", 8), ("(buffer-free wait", 14), ("dma+vmcnt+signal", 15),
+                            ("arrival wait)", 7), ("screen+tests", 9), ("insertion", 10),
+                            ("compaction", 11), ("final", 12))), flush=True)
             print(f"d={D} {mode} splits={sp}: {dt * 1e3:.2f} ms  "
                   f"{U / dt / 1e6:.2f} M users/s  {2 * U * I * D / dt / 1e12:.0f} fp32-equiv TFLOP/s",
                   flush=True)

@@ -9,6 +9,11 @@ C5  1M x 1M, 100M interactions, d=128: sampled rows of the full 3-layer forward 
     fp64 three-hop sums (1e-4); the top-20 of 512 users over all 1M items against
     torch.matmul + topk; the LGCNHS (SpreadLightGCN) top-20 of sampled users against the
     oracle's fp64 sparse restatement of F = A @ HybridS(general_W) and exact G.
+Zipf  the power-law input of SURVEY.md §8(d): Zipf(1.1) item popularity, uniform users. C4
+    shape (200K x 200K, 20M): every row of the forward against fp64; C5 shape (1M x 1M,
+    100M, d=64: hub items of ~10^6 interactions run the long-row pass): sampled rows (the
+    8 highest-degree item rows among them) against fp64 three-hop sums, and the top-20 of
+    512 users against torch.matmul + topk.
 C3 (Douban-shape SpreadLightGCNOpti, lambda = 0.5) is pinned to the reference's own run in
 test_opti_golden.py (fixture spread_opti_douban.npz).
 
@@ -210,3 +215,90 @@ def test_c5_lgcnhs_sampled_users_vs_oracle(c5, dim):
           f"tie-affected {r['tie_affected']}, mismatched {r['mismatched']}")
     assert r["mismatched"] == 0, r["first_mismatch"]
     assert r["tie_affected"] <= max(1, len(users) // 100)
+
+
+# ------------------------------------------------------------------------- Zipf(1.1)
+def test_c4_zipf_forward_every_row():
+    """Zipf(1.1) items (hubs up to ~2e5 interactions, over half of the edges on rows past the
+    long-row threshold): every row of the 3-layer mean against fp64."""
+    from lgcnhs import ops
+    from lgcnhs.graph import LONG_ROW_THRESHOLD, Adjacency
+    from lgcnhs.synth import synth_graph_device
+    U = I = 200_000
+    rowptr, src, _ = synth_graph_device(U, I, 20_000_000, seed=6, device=DEV, dist="zipf")
+    n = U + I
+    deg = (rowptr[1:] - rowptr[:-1]).cpu().numpy()
+    assert int(src.numel()) == 40_000_000 and deg.max() > 50 * LONG_ROW_THRESHOLD
+    adj = Adjacency(rowptr, src, n, n_users=U, symmetric=True)
+    e0 = torch.randn(n, 64, device=DEV, generator=torch.Generator(DEV).manual_seed(7)) * 0.1
+    out = ops.propagate(adj, e0, 3).cpu().numpy()
+    assert np.array_equal(out, ops.propagate(adj, e0, 3).cpu().numpy())  # deterministic
+    A = _csr_fp64(rowptr, src, n)
+    x = e0.cpu().numpy().astype(np.float64)
+    acc, cur = x.copy(), x
+    for _ in range(3):
+        cur = A @ cur
+        acc += cur
+    np.testing.assert_allclose(out, acc / 4, rtol=0, atol=TOL)
+
+
+@pytest.fixture(scope="module")
+def c5zipf():
+    from lgcnhs.synth import synth_graph_device
+    U = I = 1_000_000
+    rowptr, src, keys = synth_graph_device(U, I, 100_000_000, seed=3, device=DEV, dist="zipf")
+    e0 = torch.randn(U + I, 64, device=DEV, generator=torch.Generator(DEV).manual_seed(43)) * 0.1
+    return U, I, rowptr, src, keys, e0
+
+
+def test_c5_zipf_forward_sampled_rows(c5zipf):
+    """The C5-shape Zipf forward (d=64): the 8 highest-degree item rows (each ~10^6 edges:
+    the long-row pass) and 16 random rows against fp64 three-hop sums."""
+    from lgcnhs import ops
+    from lgcnhs.graph import Adjacency
+    U, I, rowptr, src, _, e0 = c5zipf
+    n = U + I
+    adj = Adjacency(rowptr, src, n, n_users=U, symmetric=True)
+    out = ops.propagate(adj, e0, 3)
+    deg = (rowptr[1:] - rowptr[:-1]).cpu().numpy()
+    hubs = U + np.argsort(-deg[U:], kind="stable")[:8]
+    rows = np.concatenate([hubs, np.random.default_rng(8).choice(n, 16, replace=False)])
+    got = out[torch.as_tensor(rows, device=DEV)].cpu().numpy()
+    del out
+    A = _csr_fp64(rowptr, src, n)
+    x = e0.cpu().numpy().astype(np.float64)
+    print(f"[C5 Zipf] hub degrees {deg[hubs].tolist()}")
+    import scipy.sparse as sp
+    for t, r in enumerate(rows):
+        v = sp.csr_matrix(([1.0], ([0], [r])), shape=(1, n))
+        acc = x[r].copy()
+        for _ in range(3):
+            v = v @ A
+            acc += (v @ x).ravel()
+        np.testing.assert_allclose(got[t], acc / 4, rtol=0, atol=TOL)
+
+
+def test_c5_zipf_top20_512_users_vs_reference_ops(c5zipf):
+    """The screened top-K over all 1M items for 512 users whose histories hold the hub items
+    (every interaction masked) against torch.matmul + -1024 index-put + torch.topk."""
+    from lgcnhs import ops
+    from lgcnhs.graph import RowSets
+    U, I, _, _, keys, e0 = c5zipf
+    nu, k = 512, 20
+    eu, ei = e0[:nu].contiguous(), e0[U:].contiguous()
+    ku = keys[keys < nu * I]
+    excl = RowSets.from_pairs(ku // I, ku % I, nu, I, DEV)
+    _, got = ops.score_topk(eu, ei, k, excl)
+    kc = ku.cpu().numpy()
+    _, ref, _ = O.recommend_topk_torch(eu.cpu(), ei.cpu(), (kc // I, kc % I), None, k)
+    eun, ein = eu.cpu().numpy(), ei.cpu().numpy()
+    ex64 = lambda u, it: ein[it].astype(np.float64) @ eun[u].astype(np.float64)  # noqa: E731
+    tol = lambda u, it: _dot_tols(eun[u], ein, it, 64)  # noqa: E731
+    ties, n = compare_topk_exact(got.cpu().numpy(), ref.numpy(), ex64, tol,
+                                 "C5 Zipf top-20 (512 users x 1M items)")
+    assert ties <= max(2, n // 100)
+    # bit-exact against the kernel's fp32 chain (C oracle) for the first 128 users as well
+    m = kc < 128 * I
+    rp, col = O.exclusion_csr(128, I, (kc[m] // I, kc[m] % I))
+    _, oi = O.chain_topk(eun[:128], ein, rp, col, k)
+    np.testing.assert_array_equal(got[:128].cpu().numpy(), oi)

@@ -97,9 +97,9 @@ def test_screened_topk_near_ties_and_wide_norms():
 @pytest.mark.parametrize("I", [3000, 40000])
 def test_screened_topk_non_finite_rows(I):
     """A NaN item row makes every user's screen margin NaN and a NaN user row its own: the
-    screen then recomputes every tile of those users exactly, so the lists stay the plain
-    kernel's bit for bit (NaN scores never enter), and finite items still fill them. At
-    40,000 items the seed pass runs too: NaN lower bounds seed nothing."""
+    screened path then hands the call to the plain kernel (non-finite margins are outside the
+    screened kernel's contract), so the lists stay the plain kernel's bit for bit (NaN scores
+    never enter), and finite items still fill them."""
     from lgcnhs import ops
     U, d, k = 64, 64, 20
     eu, ei = _emb(U, d, 41), _emb(I, d, 42)
