@@ -733,15 +733,15 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
 
 
 def topk_roofline(nu, I, D, k, tk):
-    """roofline of the screened top-K kernel (MFMA-bound): the MFMA work it executes -- the bf16
-    screen of every (user, item) and the exact fp32 chain of the (16-user group, 16-item tile)
-    pairs the screen cannot rule out -- priced in bf16-equivalent TFLOP/s (an fp32 MFMA flop
-    takes 2500 / 157.3 bf16 flops' worth of MFMA-pipe time) against the dense bf16 peak, so frac
-    is the MFMA pipe's busy fraction implied by the live time. The exact share, the PMC
-    MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES) and the HBM traffic come from
-    profiles/pmc_topk.json (scripts/gpu_r04_topk.sh + scripts/topk_pmc_summary.py), used only
-    if recorded on this csrc/topk.hip at this shape; without one, achieved counts the screen
-    alone (a lower bound) and says so."""
+    """roofline of the screened top-K (MFMA-bound): the MFMA work it executes priced against
+    the dense bf16 peak. k <= 32 (k_topk_ring, bound-side lists): the bf16 screen of every
+    (user, item) plus the seed pass's screen of the first 1/16 of the items (catalogs of >= 1024
+    k items); the exact fp32 chains run only on the ~k + 9 final entries per user and are
+    counted from the PMC record (f32 MFMAs beyond the screen's) at the bf16 / fp32 peak ratio.
+    k > 32 (k_score_topk_screen): the screen plus the recorded share of (16-user group,
+    16-item tile) pairs recomputed exactly. The record (profiles/pmc_topk.json,
+    scripts/gpu_topk_pmc.sh + scripts/topk_pmc_summary.py) is used only if taken on this
+    csrc/topk.hip at this shape; it also gives the PMC MFMA-busy fraction and HBM traffic."""
     import hashlib
     sha = hashlib.sha256(open(os.path.join(PKG, "csrc", "topk.hip"), "rb").read()).hexdigest()[:16]
     rec, status = None, f"no PMC record for c5-d{D}/topk"
@@ -756,18 +756,21 @@ def topk_roofline(nu, I, D, k, tk):
             rec, status = None, "recorded at another shape"
         else:
             status = "measured"
-    # (k <= 32 on a catalog of >= 1024 k items: the seed pass screens the first 1/16 of the
-    # items once more, csrc/topk.hip)
     seeded = k <= 32 and I // 16 // 16 * 16 >= 64 * k
     bf16 = 2.0 * nu * I * D * (1.0 + (1.0 / 16 if seeded else 0.0))
-    share = rec["exact_group_tile_share"] if rec else None
-    f32 = 2.0 * nu * I * D * share if share is not None else 0.0
+    share = rec.get("exact_group_tile_share") if rec else None
+    if k <= 32:
+        # fp32 MFMA flops of the exact chains: 16x16x4 f32 MFMA = 2048 flop each
+        f32 = 2048.0 * rec["f32_mfma_per_launch"] if rec else 0.0
+    else:
+        f32 = 2.0 * nu * I * D * share if share is not None else 0.0
     achieved = (bf16 + f32 * BF16_MFMA_PEAK_TF / F32_MFMA_PEAK_TF) / tk / 1e12
     return {"bound": "mfma", "achieved": achieved, "peak": BF16_MFMA_PEAK_TF,
             "unit": "TFLOP/s (bf16-equivalent MFMA work)", "frac": achieved / BF16_MFMA_PEAK_TF,
             "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
             "kernel": "lg_score_topk_screened_f32", "avg_launch_ms": tk * 1e3,
             "exact_group_tile_share": share,
+            "exact_f32_mfma_per_launch": rec.get("f32_mfma_per_launch") if rec else None,
             "pmc_mfma_busy_frac": rec.get("mfma_busy_frac") if rec else None,
             "pmc_avg_ms": rec.get("avg_ms") if rec else None,
             "pmc_wave_parked_frac": rec.get("wave_parked_frac") if rec else None,

@@ -256,9 +256,10 @@ class ShardedPropagation:
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 self.events.append((s, e))
-            with _WaitTimer(self.waits, l, y):
-                for h in handles:
-                    h.wait()
+            if handles:
+                with _WaitTimer(self.waits, l, y):
+                    for h in handles:
+                        h.wait()
             x = y
         if gather_out and sh.world > 1:
             for c in range(sh.chunks):
@@ -420,9 +421,10 @@ class BipartitePropagation:
             fresh = {}
             for s in order:
                 need = [1 - s] if (self.bipartite and nseg == 2) else list(pending)
-                with _WaitTimer(self.waits, l, x):
-                    for q in need:
-                        for h in pending.pop(q, []):
+                hs = [h for q in need for h in pending.pop(q, [])]
+                if hs:
+                    with _WaitTimer(self.waits, l, x):
+                        for h in hs:
                             h.wait()
                 if self.events is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
@@ -436,8 +438,9 @@ class BipartitePropagation:
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev1.record()
                     self.events.append((ev0, ev1))
-            with _WaitTimer(self.waits, l, x):
-                for hs in pending.values():  # (non-bipartite leftovers)
+            hs = [h for q in pending.values() for h in q]  # (non-bipartite leftovers)
+            if hs:
+                with _WaitTimer(self.waits, l, x):
                     for h in hs:
                         h.wait()
             pending = fresh

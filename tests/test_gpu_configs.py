@@ -228,7 +228,7 @@ def test_c4_zipf_forward_every_row():
     rowptr, src, _ = synth_graph_device(U, I, 20_000_000, seed=6, device=DEV, dist="zipf")
     n = U + I
     deg = (rowptr[1:] - rowptr[:-1]).cpu().numpy()
-    assert int(src.numel()) == 40_000_000 and deg.max() > 50 * LONG_ROW_THRESHOLD
+    assert int(src.numel()) == 40_000_000 and deg.max() > 40 * LONG_ROW_THRESHOLD
     adj = Adjacency(rowptr, src, n, n_users=U, symmetric=True)
     e0 = torch.randn(n, 64, device=DEV, generator=torch.Generator(DEV).manual_seed(7)) * 0.1
     out = ops.propagate(adj, e0, 3).cpu().numpy()
