@@ -366,6 +366,9 @@ def bench_other_graph(name, dev, steps, k, topk_users, cpu_parity=True):
             "roofline": {"bound": "hbm", "achieved": alg / k_s / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": alg / k_s / 1e9 / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": tsrc,
+                         # (hub rows' sources are re-read from L2 / the Infinity Cache: the
+                         # algorithmic rate can pass the HBM peak; the PMC bytes cannot)
+                         "traffic_frac": (traffic / k_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "kernel": "lg_spmm_layer_f32 + lg_spmm_long_rows_f32 (one layer)",
                          "avg_launch_ms": k_s * 1e3, "alg_bytes_per_launch": alg}}
     del shard
@@ -721,8 +724,9 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
     line = {"recs_per_s": nu * world / tk, "users_per_rank": nu, "items": I, "k": k, "dim": D,
             "ms": tk * 1e3, "fp32_equiv_tflops_per_gpu": flops / tk / 1e12,
             "bf16_screen_mfma_frac": flops / tk / 1e12 / BF16_MFMA_PEAK_TF,
-            "kernel": "lg_score_topk_screened_f32 (bf16 MFMA 16x16x32 screen + exact f32 "
-                      "MFMA 16x16x4 chain on the tiles it cannot rule out + streaming top-k)",
+            "kernel": "lg_score_topk_screened_f32 (bf16 MFMA 16x16x32 screen; k <= 32: "
+                      "bound-side lists ranked by the exact f32 MFMA 16x16x4 chain at the end; "
+                      "k > 32: exact chain on the tiles the screen cannot rule out)",
             "unscreened": {"ms": tp * 1e3, "recs_per_s": nu * world / tp,
                            "tflops_per_gpu": flops / tp / 1e12,
                            "mfma_frac": flops / tp / 1e12 / F32_MFMA_PEAK_TF,

@@ -83,6 +83,9 @@ def save_recs(recs: dict, path: str) -> None:
     -1 padded) that this package's main.py reads instead, so a cache file is never unpickled
     here."""
     os.makedirs(os.path.dirname(path), exist_ok=True)
+    side = lists_path(path)
+    if os.path.exists(side):  # (a failed write below never leaves an older run's lists)
+        os.remove(side)
     np.save(path, recs)
     uids = np.fromiter(recs.keys(), dtype=np.int64, count=len(recs))
     width = max((len(v) for v in recs.values()), default=0)
@@ -91,7 +94,9 @@ def save_recs(recs: dict, path: str) -> None:
     for r, v in enumerate(recs.values()):
         lists[r, :len(v)] = v
         lens[r] = len(v)
-    np.savez(lists_path(path), uids=uids, lists=lists, lens=lens)
+    tmp = side + ".tmp.npz"  # (np.savez appends .npz to names without it)
+    np.savez(tmp, uids=uids, lists=lists, lens=lens)
+    os.replace(tmp, side)  # atomic: the sidecar exists only whole, and after its .npy
 
 
 # what load_recs raises on a missing, truncated, corrupt or foreign cache file
@@ -100,8 +105,16 @@ CACHE_ERRORS = (OSError, ValueError, KeyError, EOFError, zipfile.BadZipFile)
 
 def load_recs(path: str) -> dict:
     """The dict save_recs wrote, from its pickle-free sidecar only (allow_pickle=False).
-    Raises one of CACHE_ERRORS on a missing, truncated, corrupt or foreign file."""
-    with np.load(lists_path(path), allow_pickle=False) as z:
+    The '.npy' it is named after must exist and be no newer than the sidecar: deleting the
+    '.npy' -- the reference's way to force a recompute -- invalidates the cache, and so does a
+    '.npy' rewritten after it. Raises one of CACHE_ERRORS on a missing, stale, truncated,
+    corrupt or foreign file."""
+    side = lists_path(path)
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path}: no recommendation cache (its sidecar is ignored)")
+    if os.path.getmtime(path) > os.path.getmtime(side):
+        raise ValueError(f"{side}: older than {path} (stale sidecar)")
+    with np.load(side, allow_pickle=False) as z:
         uids, lists, lens = z["uids"], z["lists"], z["lens"]
     if uids.ndim != 1 or lists.shape[0] != uids.shape[0] or lens.shape != uids.shape:
         raise ValueError(f"{lists_path(path)}: inconsistent recommendation lists")

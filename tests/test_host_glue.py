@@ -51,3 +51,24 @@ def test_saved_recs_round_trip_without_pickle(tmp_path):
         load_recs(path)
     with pytest.raises(CACHE_ERRORS):
         load_recs(str(tmp_path / "missing.npy"))
+
+
+def test_saved_recs_sidecar_follows_its_npy(tmp_path):
+    """Deleting the '.npy' (the reference's way to force a recompute) invalidates the sidecar;
+    so does a '.npy' newer than it; a rewrite replaces the sidecar whole (no old lists served
+    after a failed write)."""
+    import os
+    import pytest
+    from lgcnhs.recs import CACHE_ERRORS, lists_path, load_recs, save_recs
+    path = str(tmp_path / "rec" / "all_user_recommend_dict_LightGCN_3.npy")
+    save_recs({0: [1, 2]}, path)
+    assert load_recs(path) == {0: [1, 2]}
+    os.remove(path)
+    with pytest.raises(CACHE_ERRORS):
+        load_recs(path)
+    save_recs({0: [3]}, path)
+    assert load_recs(path) == {0: [3]} and not os.path.exists(lists_path(path) + ".tmp.npz")
+    t = os.path.getmtime(lists_path(path))
+    os.utime(path, (t + 10, t + 10))  # the .npy rewritten after its sidecar
+    with pytest.raises(CACHE_ERRORS):
+        load_recs(path)
