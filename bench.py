@@ -724,9 +724,8 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
     line = {"recs_per_s": nu * world / tk, "users_per_rank": nu, "items": I, "k": k, "dim": D,
             "ms": tk * 1e3, "fp32_equiv_tflops_per_gpu": flops / tk / 1e12,
             "bf16_screen_mfma_frac": flops / tk / 1e12 / BF16_MFMA_PEAK_TF,
-            "kernel": "lg_score_topk_screened_f32 (bf16 MFMA 16x16x32 screen; k <= 32: "
-                      "bound-side lists ranked by the exact f32 MFMA 16x16x4 chain at the end; "
-                      "k > 32: exact chain on the tiles the screen cannot rule out)",
+            "kernel": "lg_score_topk_screened_f32 (bf16 MFMA 16x16x32 screen, bound-side "
+                      "lists ranked by the exact f32 MFMA 16x16x4 chain at the end)",
             "unscreened": {"ms": tp * 1e3, "recs_per_s": nu * world / tp,
                            "tflops_per_gpu": flops / tp / 1e12,
                            "mfma_frac": flops / tp / 1e12 / F32_MFMA_PEAK_TF,
@@ -738,19 +737,19 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
 
 def topk_roofline(nu, I, D, k, tk):
     """roofline of the screened top-K (MFMA-bound): the MFMA work it executes priced against
-    the dense bf16 peak. k <= 32 (k_topk_ring, bound-side lists): the bf16 screen of every
-    (user, item) plus the seed pass's screen of the first 1/16 of the items (catalogs of >= 1024
-    k items); the exact fp32 chains run only on the ~k + 9 final entries per user and are
-    counted from the PMC record (f32 MFMAs beyond the screen's) at the bf16 / fp32 peak ratio.
-    k > 32 (k_score_topk_screen): the screen plus the recorded share of (16-user group,
-    16-item tile) pairs recomputed exactly. The record (profiles/pmc_topk.json,
+    the dense bf16 peak (k_topk_ring, bound-side lists, every k): the bf16 screen of every
+    (user, item), plus for k <= 32 the seed pass's screen of the first 1/16 of the items
+    (catalogs of >= 1024 k items); the exact fp32 chains run only on the surviving entries per
+    user (~k + 9 at k = 20) and are counted from the PMC record (f32 MFMAs beyond the screen's)
+    at the bf16 / fp32 peak ratio. The record (profiles/pmc_topk.json,
     scripts/gpu_topk_pmc.sh + scripts/topk_pmc_summary.py) is used only if taken on this
     csrc/topk.hip at this shape; it also gives the PMC MFMA-busy fraction and HBM traffic."""
     import hashlib
     sha = hashlib.sha256(open(os.path.join(PKG, "csrc", "topk.hip"), "rb").read()).hexdigest()[:16]
-    rec, status = None, f"no PMC record for c5-d{D}/topk"
+    key = f"c5-d{D}/topk" + ("" if k == 20 else f"_k{k}")
+    rec, status = None, f"no PMC record for {key}"
     try:
-        rec = json.load(open(os.path.join(REPO, "profiles", "pmc_topk.json"))).get(f"c5-d{D}/topk")
+        rec = json.load(open(os.path.join(REPO, "profiles", "pmc_topk.json"))).get(key)
     except Exception:
         rec = None
     if rec is not None:
@@ -762,18 +761,13 @@ def topk_roofline(nu, I, D, k, tk):
             status = "measured"
     seeded = k <= 32 and I // 16 // 16 * 16 >= 64 * k
     bf16 = 2.0 * nu * I * D * (1.0 + (1.0 / 16 if seeded else 0.0))
-    share = rec.get("exact_group_tile_share") if rec else None
-    if k <= 32:
-        # fp32 MFMA flops of the exact chains: 16x16x4 f32 MFMA = 2048 flop each
-        f32 = 2048.0 * rec["f32_mfma_per_launch"] if rec else 0.0
-    else:
-        f32 = 2.0 * nu * I * D * share if share is not None else 0.0
+    # fp32 MFMA flops of the exact chains: 16x16x4 f32 MFMA = 2048 flop each
+    f32 = 2048.0 * rec["f32_mfma_per_launch"] if rec else 0.0
     achieved = (bf16 + f32 * BF16_MFMA_PEAK_TF / F32_MFMA_PEAK_TF) / tk / 1e12
     return {"bound": "mfma", "achieved": achieved, "peak": BF16_MFMA_PEAK_TF,
             "unit": "TFLOP/s (bf16-equivalent MFMA work)", "frac": achieved / BF16_MFMA_PEAK_TF,
             "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
             "kernel": "lg_score_topk_screened_f32", "avg_launch_ms": tk * 1e3,
-            "exact_group_tile_share": share,
             "exact_f32_mfma_per_launch": rec.get("f32_mfma_per_launch") if rec else None,
             "pmc_mfma_busy_frac": rec.get("mfma_busy_frac") if rec else None,
             "pmc_avg_ms": rec.get("avg_ms") if rec else None,

@@ -149,7 +149,7 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
                       float mask_value, int32_t k, int32_t n_splits, float *out_val,
                       int64_t *out_idx, void *ws, size_t ws_bytes, lg_stream_t stream);
 
-/* lg_score_topk_f32 with a bf16 MFMA screen (csrc/topk.hip K2s/K2r): the same outputs bit
+/* lg_score_topk_f32 with a bf16 MFMA screen (csrc/topk.hip K2r): the same outputs bit
  * for bit (values, ids, order). eu_bf16 / ei_bf16: lg_bound_prep_f32's bf16 copies of eu / ei
  * (16-byte aligned). umarg[u] (fp32, per user) must bound |bf16 MFMA product - fp32 chain|
  * over every item, with slack for the fp32 roundings of the screen's own compares:
@@ -158,9 +158,8 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
  * (lgcnhs.ops.screen_margins, from lg_bound_prep_f32's norm_up / err_up; the round-3 form
  * 0.0081 ||eu[u]|| I is larger and also valid). Every umarg[u] must be finite (so every
  * embedding is finite and no product overflows): lgcnhs.ops routes other inputs to
- * lg_score_topk_f32. k <= 32: one pass keeps per user the items
- * whose bound can still reach the k-th largest lower bound, and ranks those by the exact chain
- * at the end; k > 32: a tile whose bound beats a user's threshold is recomputed exactly.
+ * lg_score_topk_f32. One pass keeps per user the items whose bound can still reach the k-th
+ * largest lower bound, and ranks those by the exact chain at the end (every k <= 128).
  * Workspace and splits as lg_score_topk_f32. For k <= 32 on catalogs of >= 1024 k items a
  * screen-only seed pass over the first 1/16 of the items runs first and leaves each user's
  * starting threshold in out_val[u * k + k - 1] (overwritten by the result); the outputs do

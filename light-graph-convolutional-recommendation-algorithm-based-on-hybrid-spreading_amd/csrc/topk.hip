@@ -312,16 +312,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk(
     }
   }
 }
-// K2s: the same top-K with a bf16 MFMA screen (v_mfma_f32_16x16x32_bf16, 16x the f32
-// MFMA's rate). Per 16-item tile every user's bf16 product plus a rigorous margin m_u
-// (umarg, include/lgcnhs.h: |G_bf16 - G_chain| <= m_u for every item) is an upper bound of the
-// exact fp32 chain score. Only a tile where some user's bound beats its entry threshold is
-// recomputed with the f32 MFMA chain of k_score_topk -- the exact scores, bit for bit -- and
-// runs k_score_topk's insertion on them. A tile that is not recomputed holds no score above
-// any threshold, so k_score_topk would have inserted nothing from it either: the lists
-// (values, ids, order) are k_score_topk's exactly. While a user's list can still take the
-// mask value (thr = -inf) every tile is recomputed. This per-wave kernel serves k > 32; the
-// k <= 32 lists run k_topk_ring below.
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // the largest float below a finite x
@@ -331,249 +322,10 @@ __device__ __forceinline__ float next_below(float x) {
   return __builtin_bit_cast(float, x > 0.f ? b - 1 : b + 1);
 }
 
-template <int D, int NG, int M, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
-    const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
-    const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
-    int64_t n_items, const int64_t *__restrict__ ex_rowptr,
-    const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
-    int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
-    float *__restrict__ part_val, int32_t *__restrict__ part_idx) {
-  constexpr int Q = D / 4;   // f32 MFMA steps
-  constexpr int S = D / 32;  // bf16 MFMA k-blocks
-  constexpr int CAP = 64 * M;
-  __shared__ float cs[WAVES][NG][16][CAP];
-  __shared__ int ci[WAVES][NG][16][CAP];
-  __shared__ int exs[WAVES][64];
-
-  const int wave = threadIdx.x / 64;
-  const int lane = lane_id();
-  const int ul = lane & 15;
-  const int gq = lane >> 4;
-  const int64_t tile = blockIdx.x / n_splits;
-  const int split = blockIdx.x % n_splits;
-  const int64_t ubase = (tile * WAVES + wave) * (16 * NG);
-  if (ubase >= n_users) return;  // wave-uniform; no block-level barriers below
-  const int64_t i0 = (int64_t)split * items_per_split;
-  int64_t i1 = i0 + items_per_split;
-  if (i1 > n_items) i1 = n_items;
-  const int n_valid = i1 > i0 ? (int)(i1 - i0) : 0;
-  const int n_t = (n_valid + 15) / 16;
-
-  float uf[NG][Q];
-  bf16x8 ub[NG][S];
-  float marg[NG];
-  bool uvalid[NG];
-  int64_t ex_pos[NG], ex_hi[NG];
-  int cnt[NG], chk[NG];
-  float tau[NG], thr[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int64_t u = ubase + g * 16 + ul;
-    uvalid[g] = u < n_users;
-    const int64_t uu = uvalid[g] ? u : n_users - 1;
-    load_piece<Q>(eu + uu * D + gq * Q, uf[g]);
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
-    marg[g] = umarg[uu];
-    ex_pos[g] = 0;
-    ex_hi[g] = 0;
-    if (ex_rowptr && uvalid[g]) {
-      ex_pos[g] = ex_rowptr[u];
-      ex_hi[g] = ex_rowptr[u + 1];
-    }
-    cnt[g] = 0;
-    chk[g] = 0;
-    tau[g] = neg_inf<float>();
-    thr[g] = uvalid[g] ? neg_inf<float>() : __builtin_huge_valf();
-  }
-  const uint64_t same_user = 0x0001000100010001ull << ul;
-  // retire the prologue loads with a wait hipcc sees (vmcnt(0)): otherwise its waitcnt pass
-  // merges their pending state into the loop header and waits for them inside the loop
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  // compact (and raise the threshold) once k + 12 candidates are held: the screen's hit
-  // rate follows the threshold
-  const int trig = k + 12 < CAP - 16 ? k + 12 : CAP - 16;
-
-  // (k_score_topk's lazy exclusion and compaction, unchanged)
-  auto compact_user = [&](int g, int u, int lim) __attribute__((always_inline)) {
-    const int n = __shfl(cnt[g], u);
-    const int c0 = __shfl(chk[g], u);
-    int64_t pos = __shfl(ex_pos[g], u);
-    const int64_t hi = __shfl(ex_hi[g], u);
-    float *ks = &cs[wave][g][u][0];
-    int *is = &ci[wave][g][u][0];
-    if (n > c0) {
-      while (pos < hi) {
-        const int64_t e = pos + lane;
-        const int32_t x = e < hi ? ex_col[e] : 0x7fffffff;
-        const int nin = __popcll(__ballot(x < lim));
-        if (nin == 0) break;
-        exs[wave][lane] = x;
-        wave_sync();
-        for (int j = c0 + lane; j < n; j += 64) {
-          const int item = is[j];
-          int a = 0, b = nin;
-          while (a < b) {
-            const int mid = (a + b) >> 1;
-            if (exs[wave][mid] < item) a = mid + 1;
-            else b = mid;
-          }
-          if (a < nin && exs[wave][a] == item) ks[j] = mask_value;
-        }
-        wave_sync();
-        pos += nin;
-        if (nin < 64) break;
-      }
-    }
-    float t;
-    int tid;
-    const int nc = wave_compact<float, M>(ks, is, n, k, t, tid);
-    if (ul == u) {
-      cnt[g] = nc;
-      chk[g] = nc;
-      tau[g] = t;
-      ex_pos[g] = pos;
-      thr[g] = !uvalid[g] ? __builtin_huge_valf() : (mask_value > t ? neg_inf<float>() : t);
-    }
-  };
-  auto maybe_compact = [&](int lim) __attribute__((always_inline)) {
-    bool over = false;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) over |= cnt[g] > trig;
-    if (__ballot(over) == 0) return;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      uint64_t need = __ballot(cnt[g] > trig) & 0xffffull;
-      if (need) {
-        wave_sync();
-        while (need) {
-          const int u = __ffsll((long long)need) - 1;
-          need &= need - 1;
-          compact_user(g, u, lim);
-        }
-      }
-    }
-  };
-  // bf16 fragments of tile t: lane (ul, gq) holds item ul's elements 32 s + 8 gq .. + 7
-  auto load_bf = [&](int t, bf16x8 (&fr)[S]) __attribute__((always_inline)) {
-    int64_t it = i0 + 16 * t + ul;
-    it = it < n_items ? it : n_items - 1;
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      fr[s] = *reinterpret_cast<const bf16x8 *>(eib + it * D + 32 * s + 8 * gq);
-  };
-  // insertion of tile t's exact scores acc[g] (lane (ul, gq): item 4 gq + r of the tile,
-  // user ul) into the lists of the groups gh, against thr
-  auto insert_acc = [&](int t, const bool (&gh)[NG], const f32x4 (&accs)[NG])
-      __attribute__((always_inline)) {
-    const int rel = t * 16 + gq * 4;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (!gh[g]) continue;
-      const f32x4 acc = accs[g];
-      if (__ballot(above(max4(acc), thr[g])) == 0) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float sc = acc[r];
-        const bool cand = rel + r < n_valid && sc > thr[g];
-        const uint64_t bal = __ballot(cand);
-        if (bal) {
-          const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
-          if (cand) {
-            cs[wave][g][ul][pos] = sc;
-            ci[wave][g][ul][pos] = (int)i0 + rel + r;
-          }
-          cnt[g] += __popcll(bal & same_user);
-        }
-      }
-    }
-  };
-  // the exact tile: k_score_topk's f32 chain (only the user groups whose screen hit: a
-  // group's chain is its own 16-user MFMA column block), then its insertion against thr
-  auto exact_tile = [&](int t, const bool (&gh)[NG]) __attribute__((always_inline)) {
-    float af[Q];
-    int64_t it = i0 + 16 * t + ul;
-    it = it < n_items ? it : n_items - 1;
-    load_piece<Q>(ei + it * D + gq * Q, af);
-    f32x4 accs[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!gh[g]) continue;  // (wave-uniform)
-#pragma unroll
-      for (int s = 0; s < Q; ++s)
-        accs[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], uf[g][s], accs[g], 0, 0, 0);
-    }
-    insert_acc(t, gh, accs);
-  };
-
-  const int lim_end = (int)i1;
-  // two tiles' bf16 fragments in flight. Every load is issued (clamped past the end): with
-  // the tile t + 2 load conditional, hipcc's vmcnt bookkeeping followed the path without it
-  // and the wait before tile t + 1 drained tile t + 2's loads as well (23.7 -> 18.6 ms at
-  // C5, d = 64; deeper rings measured no faster, profiles/r03_topk_ring_ab.log)
-  bf16x8 fr[2][S];
-  load_bf(0, fr[0]);
-  load_bf(1, fr[1]);
-  for (int t0 = 0; t0 < n_t; t0 += 2) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int t = t0 + p;
-      if (t >= n_t) break;
-      f32x4 accb[NG];
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        accb[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-          accb[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[p][s], ub[g][s], accb[g], 0, 0, 0);
-      }
-      load_bf(t + 2, fr[p]);  // tile t + 2 into the buffer tile t just left
-      bool gh[NG];
-      bool hit = false;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        // (a NaN bound, e.g. from a non-finite embedding or margin, recomputes the tile)
-        gh[g] = __ballot(above(max4(accb[g]) + marg[g], thr[g])) != 0;
-        hit |= gh[g];
-      }
-      if (hit) {
-        exact_tile(t, gh);
-        const int l = (int)i0 + (t + 1) * 16;
-        maybe_compact(l < lim_end ? l : lim_end);
-      }
-    }
-  }
-
-  wave_sync();
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    for (int u = 0; u < 16; ++u) {
-      const int64_t user = ubase + g * 16 + u;
-      if (user >= n_users) break;
-      compact_user(g, u, lim_end);
-      const int nc = __shfl(cnt[g], u);
-      for (int e = lane; e < k; e += 64) {
-        const float v = e < nc ? cs[wave][g][u][e] : neg_inf<float>();
-        const int id = e < nc ? ci[wave][g][u][e] : -1;
-        if (n_splits == 1) {
-          out_val[user * k + e] = v;
-          out_idx[user * k + e] = id;
-        } else {
-          const int64_t o = ((int64_t)split * n_users + user) * k + e;
-          part_val[o] = v;
-          part_idx[o] = id;
-        }
-      }
-      wave_sync();
-    }
-  }
-}
-
-// K2r: the screened top-K for k <= 32, with bound-side lists -- no exact score inside the
-// streaming loop.
+// K2r: the screened top-K (every k <= 128), with bound-side lists -- no exact score inside
+// the streaming loop. A bf16 MFMA product (v_mfma_f32_16x16x32_bf16, 16x the f32 MFMA's rate)
+// plus a rigorous per-user margin m_u (umarg, include/lgcnhs.h: |G_bf16 - G_chain| <= m_u for
+// every item) bounds the exact fp32 chain score of k_score_topk from both sides.
 //
 // Every item i of user u has, from its bf16 product b = G_bf16(u, i), a lower bound
 // LB = fl(b - m_u) and an upper bound UB = fl(b + m_u) of its exact chain score (nudged
@@ -588,12 +340,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_score_topk_screen(
 // k_score_topk's. If a compaction leaves more entries than a tile could still add room for,
 // the entries are made exact right there (the same chain) and the list cut to k.
 // The loop thus issues no load but the fragment ring's DMA, and a hit costs an insertion
-// instead of a global fp32 load round trip + a chain (round 4's K2s kept ~70 % of its time in
-// those). The cost: a few more entries per list -- those within 2 m_u of the k-th value --
+// instead of a global fp32 load round trip + a chain (round 4's exact-tile kernel kept ~70 %
+// of its time in those). The cost: a few more entries per list -- those within 2 m_u of the k-th value --
 // which the tight per-user margin keeps small (~k + 9 at C5, d = 64).
 //
 // The item fragments are shared by the block's waves through LDS, as the fragment ring
-// described at the loop; lists live in LDS (CAP entries per user, one per lane).
+// described at the loop; lists live in LDS (CAP entries per user, M per lane).
 // Seeded thresholds. In a streaming top-K most insertions happen early: k ln(N / k) of them
 // over N items, three quarters within the first 1/16 of the range. So a first, screen-only pass
 // (SEEDP) over the first 1/16 of the items keeps, per user, the largest LB of each of C classes
@@ -658,7 +410,7 @@ __device__ unsigned long long g_topk_counts[16];
 #define LG_RING_NG 2
 #endif
 
-template <int D, int NG, int WAVES, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
+template <int D, int NG, int WAVES, int M, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
 __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
     const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
@@ -667,11 +419,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
     float *__restrict__ part_val, int32_t *__restrict__ part_idx,
     const float *__restrict__ seed_val) {
-  // WAVES waves x NG groups of 16 users (the MFMA columns): 256 users per CU
-  static_assert(NG * WAVES * 16 == 256, "256 users per block");
+  // WAVES waves x NG groups of 16 users (the MFMA columns); a list of CAP entries per user, M
+  // per lane (entry e = 64 j + lane in slab j). The host picks CAP >= k + 16 + the tile's 16
+  // (k <= 32: 256 users and CAP 56; k <= 64: 128 users and CAP 112; k <= 128: 64 users and
+  // CAP 224 -- 112 KiB of lists in each)
+  static_assert(M == 1 || M == 2 || M == 4, "list slabs");
+  static_assert(CAP <= 64 * M && CAP >= 48 * M, "list capacity");
+  static_assert(!SEEDP || M == 1, "the seed pass serves k <= 32");
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
-  static_assert(CAP <= 64 && CAP >= 48, "one list entry per lane, room for k + a tile");
   // the fragment ring: chunks of CI items (CB bytes, PPT 16-byte LDS-DMA pieces per thread)
   constexpr int CB = D >= 64 || WAVES >= 8 ? 8192 : 4096;  // (>= one 16-byte piece per thread)
   constexpr int CI = CB / (2 * D), TPC = CI / 16, PR = D / 8, RB = 2 * D;
@@ -757,12 +513,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   // The exact chain scores of the list entries of user `user` on the lanes in `want` (lane e:
   // entry e, item `item`): k_score_topk's f32 MFMA chain with 16 entries as the A rows and the
   // user in every B column, so column ul of the result is the chain of (user, entry) bit for
-  // bit. Results pass through exs (lane e reads its own).
+  // bit. One slab of a list per call (lane e: entry 64 j + e); results pass through exs (lane
+  // e reads its own).
   auto exact_entries = [&](int64_t user, uint64_t want, int item) __attribute__((always_inline)) {
     float uf[Q];
     user = user < n_users ? user : n_users - 1;  // (callers pass valid users; a clamp is cheap)
     load_piece<Q>(eu + user * D + gq * Q, uf);
-    constexpr int NB = CAP / 16 + (CAP % 16 ? 1 : 0);  // 16-entry batches
+    constexpr int CS = CAP < 64 ? CAP : 64;            // entries of one slab
+    constexpr int NB = CS / 16 + (CS % 16 ? 1 : 0);    // 16-entry batches
     constexpr int BL = D <= 64 ? 4 : 2;               // batches whose rows load together
 #pragma unroll
     for (int b0 = 0; b0 < NB; b0 += BL) {
@@ -806,11 +564,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   // per group and tile -- inlined copies made the kernel ~54 KB of code)
   // (an explicit conditional chain: a helper taking the array by reference kept the per-group
   // arrays in scratch memory -- private segment 128 B/lane -- instead of registers)
-  static_assert(NG == 2 || NG == 4, "gget's chains");
+  static_assert(NG == 1 || NG == 2 || NG == 4, "gget's chains");
 #define gget(a, g)                                                                              \
-  (NG == 2 ? ((g) ? (a)[1 % NG] : (a)[0])                                                       \
-           : ((g) == 0 ? (a)[0] : (g) == 1 ? (a)[1 % NG] : (g) == 2 ? (a)[2 % NG] : (a)[3 % NG]))
-  auto compact_user = [&](int g, int u, int lim, bool fin, float &ov, int &oi)
+  (NG == 1   ? (a)[0]                                                                           \
+   : NG == 2 ? ((g) ? (a)[1 % NG] : (a)[0])                                                     \
+             : ((g) == 0 ? (a)[0] : (g) == 1 ? (a)[1 % NG] : (g) == 2 ? (a)[2 % NG] : (a)[3 % NG]))
+  auto compact_user = [&](int g, int u, int lim, bool fin, float (&ov)[M], int (&oi)[M])
       __attribute__((always_inline)) {
     const int n = __shfl(gget(cnt, g), u);
     const int c0 = __shfl(gget(chk, g), u);
@@ -828,17 +587,21 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         if (nin == 0) break;
         exs[wave][lane] = x;
         wave_sync();
-        if (lane >= c0 && lane < n) {
-          const int item = (int)is[lane];  // (entries since the last compaction: not final)
-          int a = 0, b = nin;              // first index with exs[] >= item
-          while (a < b) {
-            const int mid = (a + b) >> 1;
-            if (exs[wave][mid] < item) a = mid + 1;
-            else b = mid;
-          }
-          if (a < nin && exs[wave][a] == item) {
-            ks[lane] = mask_value;
-            is[lane] = (uint32_t)item | kFinal;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const int ej = 64 * j + lane;
+          if (ej >= c0 && ej < n) {
+            const int item = (int)is[ej];  // (entries since the last compaction: not final)
+            int a = 0, b = nin;            // first index with exs[] >= item
+            while (a < b) {
+              const int mid = (a + b) >> 1;
+              if (exs[wave][mid] < item) a = mid + 1;
+              else b = mid;
+            }
+            if (a < nin && exs[wave][a] == item) {
+              ks[ej] = mask_value;
+              is[ej] = (uint32_t)item | kFinal;
+            }
           }
         }
         wave_sync();
@@ -846,53 +609,89 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         if (nin < 64) break;
       }
     }
-    const bool have = lane < n;
-    const float key = have ? ks[lane] : 0.f;
-    const uint32_t idr = have ? is[lane] : 0u;
-    const bool isfin = (idr & kFinal) != 0;
-    const int item = (int)(idr & ~kFinal);
-    float lb = isfin ? key : lbound(key, m);
-    float hb = isfin ? key : ubound(key, m);
-    lb = lb == lb ? lb : neg_inf<float>();           // (NaN: no lower bound)
-    hb = hb == hb ? hb : __builtin_huge_valf();      // (NaN: no upper bound)
+    bool have[M], isfin[M], keep[M];
+    float key[M], lb[M], hb[M];
+    uint32_t idr[M];
+    int item[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int ej = 64 * j + lane;
+      have[j] = ej < n;
+      key[j] = have[j] ? ks[ej] : 0.f;
+      idr[j] = have[j] ? is[ej] : 0u;
+      isfin[j] = (idr[j] & kFinal) != 0;
+      item[j] = (int)(idr[j] & ~kFinal);
+      lb[j] = isfin[j] ? key[j] : lbound(key[j], m);
+      hb[j] = isfin[j] ? key[j] : ubound(key[j], m);
+      lb[j] = lb[j] == lb[j] ? lb[j] : neg_inf<float>();       // (NaN: no lower bound)
+      hb[j] = hb[j] == hb[j] ? hb[j] : __builtin_huge_valf();  // (NaN: no upper bound)
+    }
     float tau = neg_inf<float>();
-    if (n >= k) {  // the k-th largest LB: greatest T with k lanes at or above it
-      const uint32_t o = ford(lb);
+    if (n >= k) {  // the k-th largest LB: greatest T with k entries at or above it
+      uint32_t o[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) o[j] = ford(lb[j]);
       uint32_t T = 0u;
 #pragma unroll 4
       for (int b = 31; b >= 0; --b) {
         const uint32_t c = T | (1u << b);
-        if (__popcll(__ballot(have && o >= c)) >= k) T = c;
+        int nc = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) nc += __popcll(__ballot(have[j] && o[j] >= c));
+        if (nc >= k) T = c;
       }
       tau = funord(T);
     }
-    const bool keep = have && hb >= fmaxf(tau, st);
-    const uint64_t kb = __ballot(keep);
-    int nk = __popcll(kb);
-    wave_sync();  // (every lane has read its entry)
+    uint64_t kb[M];
+    int nk = 0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      keep[j] = have[j] && hb[j] >= fmaxf(tau, st);
+      kb[j] = __ballot(keep[j]);
+      nk += __popcll(kb[j]);
+    }
+    wave_sync();  // (every lane has read its entries)
     LG_COUNT(2, fin ? 0 : 1);
     LG_COUNT(3, (!fin && nk > CAP - 16) ? 1 : 0);
     LG_COUNT(5, fin ? nk : 0);
     LG_COUNT(6, fin ? 1 : 0);
     if (fin || nk > CAP - 16) {
-      const float raw = exact_entries(ubase + g * 16 + u, kb, item);
-      const bool ok = keep && raw == raw && raw > neg_inf<float>();
-      float kk[1] = {ok ? (isfin ? key : raw) : neg_inf<float>()};
-      int ii[1] = {ok ? item : kPadId};
-      wave_bitonic_sort<float, 1>(kk, ii);
-      nk = __popcll(__ballot(ok));
-      nk = nk < k ? nk : k;
-      if (lane < nk) {
-        ks[lane] = kk[0];
-        is[lane] = (uint32_t)ii[0] | kFinal;
+      float kk[M];
+      int ii[M];
+      int nok = 0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const float raw = kb[j] ? exact_entries(ubase + g * 16 + u, kb[j], item[j]) : 0.f;
+        const bool ok = keep[j] && raw == raw && raw > neg_inf<float>();
+        kk[j] = ok ? (isfin[j] ? key[j] : raw) : neg_inf<float>();
+        ii[j] = ok ? item[j] : kPadId;
+        nok += __popcll(__ballot(ok));
       }
-      tau = nk == k ? __shfl(kk[0], k - 1) : neg_inf<float>();
-      ov = lane < nk ? kk[0] : neg_inf<float>();
-      oi = lane < nk ? ii[0] : -1;
-    } else if (keep) {
-      const int p = __popcll(kb & lanemask_lt());
-      ks[p] = key;
-      is[p] = idr;
+      wave_bitonic_sort<float, M>(kk, ii);
+      nk = nok < k ? nok : k;
+      tau = neg_inf<float>();
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const int ej = 64 * j + lane;
+        if (ej < nk) {
+          ks[ej] = kk[j];
+          is[ej] = (uint32_t)ii[j] | kFinal;
+        }
+        if (nk == k && j == ((k - 1) >> 6)) tau = __shfl(kk[j], (k - 1) & 63);  // (uniform)
+        ov[j] = ej < nk ? kk[j] : neg_inf<float>();
+        oi[j] = ej < nk ? ii[j] : -1;
+      }
+    } else {
+      int base = 0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        if (keep[j]) {
+          const int p = base + __popcll(kb[j] & lanemask_lt());
+          ks[p] = key[j];
+          is[p] = idr[j];
+        }
+        base += __popcll(kb[j]);
+      }
     }
     wave_sync();
     const float nthr = entry_thr(tau, st);
@@ -916,8 +715,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     return need;
   };
   auto compact_one = [&](int b, int lim) __attribute__((always_inline)) {
-    float ov;
-    int oi;
+    float ov[M];
+    int oi[M];
     compact_user(b >> 4, b & 15, lim, false, ov, oi);
   };
   auto compact_over = [&](int lim) __attribute__((always_inline)) {
@@ -987,15 +786,30 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     // before every LDS read, as it cannot tell the ring's buffers apart); an untracked load
     // only makes hipcc's own vmcnt waits stricter (the counter retires in order).
     auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
-    auto dma = [&](int c) __attribute__((always_inline)) {
+    // this thread's DMA source for chunk 0 (element offset), and the last chunk whose rows all
+    // lie inside the table: past it the rows are clamped per lane (harmless reads)
+    int64_t src0[PPT];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = 64 * WAVES * j + (int)threadIdx.x, r = p / PR;
+      src0[j] = (i0 + r) * D + 8 * ((p % PR) ^ sw(r));
+    }
+    const int64_t c_full = (n_items - i0) / CI - 1;  // chunks c <= c_full need no clamp
+    // buffer b (= c % NBUF) of chunk c
+    auto dma = [&](int c, int b) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < PPT; ++j) {
-        const int p = 64 * WAVES * j + (int)threadIdx.x, r = p / PR;
-        int64_t it = i0 + (int64_t)c * CI + r;
-        it = it < n_items ? it : n_items - 1;  // (past the split or the table: harmless reads)
-        const __bf16 *src = eib + it * D + 8 * ((p % PR) ^ sw(r));
+        const __bf16 *src;
+        if (c <= c_full) {  // (wave-uniform)
+          src = eib + src0[j] + (int64_t)c * CI * D;
+        } else {
+          const int p = 64 * WAVES * j + (int)threadIdx.x, r = p / PR;
+          int64_t it = i0 + (int64_t)c * CI + r;
+          it = it < n_items ? it : n_items - 1;  // (past the split or the table)
+          src = eib + it * D + 8 * ((p % PR) ^ sw(r));
+        }
         const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(
-            __attribute__((address_space(3))) char *)(frs[c % NBUF] + 1024 * (WAVES * j + wave)));
+            __attribute__((address_space(3))) char *)(frs[b] + 1024 * (WAVES * j + wave)));
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -1028,8 +842,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     };
     typedef bf16x8 Frags[TPC][S];
     typedef f32x4 Accs[TPC][NG];
-    auto read_chunk = [&](int c, Frags &fr) __attribute__((always_inline)) {
-      const char *fb = frs[c % NBUF];
+    auto read_chunk = [&](int b, Frags &fr) __attribute__((always_inline)) {
+      const char *fb = frs[b];
 #pragma unroll
       for (int tt = 0; tt < TPC; ++tt) {
         const int r = 16 * tt + ul;
@@ -1140,11 +954,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const int n_c = (n_t + TPC - 1) / TPC;  // (block-uniform)
     if (threadIdx.x < WAVES) prog[threadIdx.x] = 0u;
     __syncthreads();  // (the only block barrier)
-    for (int c = 0; c < LA; ++c) dma(c);
+    for (int c = 0; c < LA; ++c) dma(c, c);
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG * PPT) : "memory");
     landed = LA - LAG;
     publish();
     pv_ = read_prog();
+    int bc = 0, bn = LA;  // the buffers of chunks c and c + LA (running, no divisions)
     for (int c = 0; c < n_c; ++c) {
       LG_CLK0(t_ring);
       {
@@ -1152,7 +967,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         if (cp >= 0) wait_reached(pv_, (uint32_t)(cp + 1), 16);
         LG_CLK1(14, t_ring);
         LG_CLK0(t_dma);
-        dma(cn);  // (chunks past the split: harmless clamped reads, published like the rest)
+        dma(cn, bn);  // (chunks past the split: harmless clamped reads, published like the rest)
+        bn = bn + 1 == NBUF ? 0 : bn + 1;
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LAG * PPT) : "memory");
         landed = (uint32_t)(cn - LAG + 1);
         LG_CLK1(15, t_dma);
@@ -1167,7 +983,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       // instead of one tile's LDS -> MFMA -> compare chain at a time.
       Frags fr;
       Accs acc;
-      read_chunk(c, fr);
+      read_chunk(bc, fr);
+      bc = bc + 1 == NBUF ? 0 : bc + 1;
       mfma_chunk(fr, acc);
       // (the fragments are in registers: the buffer is free) -- published with this chunk's
       // landed count, and the next check's read issued right away
@@ -1239,17 +1056,21 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     {
       const int64_t user = ubase + b;
       if (user >= n_users) break;
-      float v;
-      int id;
+      float v[M];
+      int id[M];
       compact_user(b >> 4, b & 15, lim_end, true, v, id);
-      if (lane < k) {
-        if (n_splits == 1) {
-          out_val[user * k + lane] = v;
-          out_idx[user * k + lane] = id;
-        } else {
-          const int64_t o = ((int64_t)split * n_users + user) * k + lane;
-          part_val[o] = v;
-          part_idx[o] = id;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const int ej = 64 * j + lane;
+        if (ej < k) {
+          if (n_splits == 1) {
+            out_val[user * k + ej] = v[j];
+            out_idx[user * k + ej] = id[j];
+          } else {
+            const int64_t o = ((int64_t)split * n_users + user) * k + ej;
+            part_val[o] = v[j];
+            part_idx[o] = id[j];
+          }
         }
       }
     }
@@ -1458,32 +1279,23 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
                                  float *part_val, int32_t *part_idx, const float *seed_val,
                                  hipStream_t stream) {
-#define LG_SCREEN_LAUNCH(NG, MM, W)                                                           \
+  // one block per CU: 112 KiB of lists + the fragment ring. k <= 32: 256 users of CAP
+  // LG_RING_CAP; k <= 64: 128 users (8 waves x 1 group) of CAP 112; k <= 128: 64 users (4 waves
+  // x 1 group) of CAP 224
+#define LG_RING_LAUNCH(NG, W, MM, CAP, SEEDP)                                                 \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_score_topk_screen<D, NG, MM, W>                                                         \
+    k_topk_ring<D, NG, W, MM, CAP, LG_RING_NBUF, LG_RING_LA, LG_RING_LAG, SEEDP>              \
         <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
-            eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
-            n_splits, items_per_split, out_val, out_idx, part_val, part_idx);                 \
-  }
-  // k <= 32: one block per CU (RING_CAP-entry lists for 256 users + the fragment ring)
-  // shares the item fragments; larger lists keep 2-wave blocks that load their own
-#define LG_RING_LAUNCH(SEEDP)                                                                 \
-  {                                                                                           \
-    const int64_t tiles = (n_users + 255) / 256;                                              \
-    k_topk_ring<D, LG_RING_NG, 16 / LG_RING_NG, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,         \
-                LG_RING_LAG, SEEDP>                                                           \
-        <<<dim3((unsigned)(tiles * n_splits)), dim3(1024 / LG_RING_NG), 0, stream>>>(         \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
-  if (M == 1 && seedp) LG_RING_LAUNCH(true)
-  else if (M == 1) LG_RING_LAUNCH(false)
-  else if (M == 2) LG_SCREEN_LAUNCH(2, 2, 2)
-  else LG_SCREEN_LAUNCH(1, 4, 2)
+  if (M == 1 && seedp) LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, true)
+  else if (M == 1) LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, false)
+  else if (M == 2) LG_RING_LAUNCH(1, 8, 2, 112, false)
+  else LG_RING_LAUNCH(1, 4, 4, 224, false)
 #undef LG_RING_LAUNCH
-#undef LG_SCREEN_LAUNCH
 }
 
 static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }

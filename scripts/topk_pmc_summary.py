@@ -1,17 +1,17 @@
 """Summarise scripts/gpu_topk_pmc.sh (rocprofv3 kernel trace + PMC passes over the screened
-top-K at C5: 32768 users x 1M items, k = 20, d = 64 and 128) into profiles/pmc_topk.json,
-keyed "c5-d<D>/topk", with the hash of csrc/topk.hip (bench.py uses a record only for the
+top-K at C5: 32768 users x 1M items, k = 20 (or K), d = 64 and 128) into
+profiles/pmc_topk.json, keyed "c5-d<D>/topk" (k = 20) or "c5-d<D>/topk_k<K>", with the hash of csrc/topk.hip (bench.py uses a record only for the
 source it was measured on).
 
-The k <= 32 kernel is k_topk_ring<D, NG, WAVES, CAP, NBUF, LA, LAG, SEEDP> (csrc/topk.hip K2r):
-a seed pass (SEEDP = true, the first 1/16 of the items) then the main pass. Per call: the
+The kernel is k_topk_ring<D, NG, WAVES, M, CAP, NBUF, LA, LAG, SEEDP> (csrc/topk.hip K2r): for
+k <= 32 a seed pass (SEEDP = true, the first 1/16 of the items), then the main pass. Per call: the
 kernels' average durations, SQ_VALU_MFMA_BUSY_CYCLES as a fraction of the SIMD cycles
 (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) of the main pass, its instruction mix per wave and per
 64-item chunk, the wave-state split (SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over
 SQ_WAVE_CYCLES) and HBM traffic (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 corrections of
 MI355X_MICROARCH.md). The bf16 MFMAs beyond the screen's (waves x chunks x 16 at d = 64) are
 the f32 MFMAs of the exact chains (the final ranking and mid-stream escapes).
-Usage: python scripts/topk_pmc_summary.py TAG DIR"""
+Usage: python scripts/topk_pmc_summary.py TAG DIR [K]"""
 import csv
 import hashlib
 import json
@@ -22,10 +22,10 @@ from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 USERS, ITEMS, K = 32768, 1_000_000, 20
-PAT = r"k_topk_ring<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, (true|false)>"
+PAT = r"k_topk_ring<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, \d+, (true|false)>"
 
 
-def main(tag, d):
+def main(tag, d, K=K):
     dur = defaultdict(list)
     seed_dur = defaultdict(list)
     for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))):
@@ -57,7 +57,7 @@ def main(tag, d):
         users_per_wave = 16 * NG
         items_per_wave = ITEMS * users_per_wave * waves / USERS / waves  # (the wave's split)
         splits = waves * users_per_wave / USERS
-        chunk_items = 8192 // (2 * D)
+        chunk_items = (8192 if D >= 64 or WAVES >= 8 else 4096) // (2 * D)
         chunks = ITEMS / splits / chunk_items
         bf16_mfma = waves * chunks * (chunk_items // 16) * NG * (D // 32)
         f32_mfma = max(0.0, avg["SQ_INSTS_MFMA"] - bf16_mfma)
@@ -83,10 +83,10 @@ def main(tag, d):
              "clock_ghz_profiled": avg["GRBM_GUI_ACTIVE"] / 8 / (md * 1e6) if md else None,
              "hbm_bytes_per_launch": (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024,
              "counters_per_launch": avg}
-        out[f"c5-d{D}/topk"] = e
+        out[f"c5-d{D}/topk" + ("" if K == 20 else f"_k{K}")] = e
         print(json.dumps({k: v for k, v in e.items() if k != "counters_per_launch"}, indent=1))
     json.dump(out, open(tp, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(int(a) for a in sys.argv[3:4]))

@@ -74,7 +74,7 @@ def test_topk_roofline_prices_the_screen_the_seed_pass_and_the_exact_chains():
     assert abs(r["frac"] - want / bench.BF16_MFMA_PEAK_TF) < 1e-12
     # k > 32: no seed pass; a shape without a record: the screen alone, flagged
     r2 = bench.topk_roofline(nu, I, D, 33, t)
-    assert r2["exact_group_tile_share"] is None
+    assert r2["exact_f32_mfma_per_launch"] is None
     assert r2["record_source"]["status"] != "measured"
     assert abs(r2["achieved"] - base / t / 1e12) < 1e-9 * r2["achieved"]
 

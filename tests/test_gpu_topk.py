@@ -70,13 +70,14 @@ def test_score_topk_bit_exact(d, k, screen):
         assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
-def test_screened_topk_near_ties_and_wide_norms():
+@pytest.mark.parametrize("k", [20, 64, 100, 128])
+def test_screened_topk_near_ties_and_wide_norms(k):
     """The bf16 screen's margin under stress: items that differ below bf16 resolution (their
     bf16 products tie, the fp32 chain orders them), scaled items and users over 1e-3..1e2,
     a zero user row: the screened lists equal the plain kernel's and the oracle's bit for
-    bit."""
+    bit (k = 64 / 100 / 128: lists of 2 and 4 slabs per lane, escapes among the near-copies)."""
     from lgcnhs import ops
-    U, I, d, k = 96, 5000, 64, 20
+    U, I, d = 96, 5000, 64
     eu, ei = _emb(U, d, 31), _emb(I, d, 32)
     base = ei[:40].clone()
     for r in range(1, 8):  # 7 near-copies of 40 items, each off by a sub-bf16 perturbation
@@ -170,10 +171,11 @@ def test_score_topk_edge_cases():
                                                                   None, None, 3)[1])
 
 
-def test_score_topk_large_catalog_sample():
+@pytest.mark.parametrize("k", [20, 100])
+def test_score_topk_large_catalog_sample(k):
     """1M-item catalog (the C5 item count), 256 users: bit-exact vs the C oracle."""
     from lgcnhs import ops
-    U, I, k = 256, 1_000_000, 20
+    U, I = 256, 1_000_000
     eu, ei = _emb(U, 64, 7), _emb(I, 64, 8)
     rp, col = _excl(U, I, 1e-4, 9)
     ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
