@@ -376,7 +376,30 @@ __device__ __forceinline__ float ubound(float b, float m) {
   return e + (fabsf(e) * 0x1p-22f + 1e-30f);
 }
 
-constexpr uint32_t kFinal = 0x80000000u;  // list entry id bit: the key is the final value
+// List entries are 6 bytes: a 32-bit key and the item's 16-bit tile index in its split (so a
+// split holds at most 2^20 items). The key is a float whose 6 low mantissa bits are replaced:
+// bits 0-3 the item's row in its tile, bit 4 kExact (the key is the exact chain score, LB = UB
+// up to the truncation), bit 5 kExcl (an excluded item: its final value is the mask value
+// exactly). Clearing 6 low bits moves a float by < 64 ulp <= 2^-17 |key| (toward zero), which
+// the bounds widen by: lbound_t / ubound_t below.
+constexpr uint32_t kRowMask = 15u, kExact = 16u, kExcl = 32u, kLowBits = 63u;
+constexpr int kTileBits = 16;  // tile index field: splits of at most 2^20 items
+__device__ __forceinline__ float key_value(uint32_t kb) {
+  return __builtin_bit_cast(float, kb & ~kLowBits);
+}
+__device__ __forceinline__ uint32_t key_pack(float v, uint32_t low) {
+  return (__builtin_bit_cast(uint32_t, v) & ~kLowBits) | low;
+}
+// bounds of the true value from a truncated key v = key_value(kb): widened by |v| 2^-16 (> the
+// truncation's 2^-17 |v| and the roundings of the sum)
+__device__ __forceinline__ float lbound_t(float v, float m) {
+  const float d = v - m;
+  return d - (fabsf(d) * 0x1p-22f + fabsf(v) * 0x1p-16f + 1e-30f);
+}
+__device__ __forceinline__ float ubound_t(float v, float m) {
+  const float e = v + m;
+  return e + (fabsf(e) * 0x1p-22f + fabsf(v) * 0x1p-16f + 1e-30f);
+}
 
 #ifdef LG_TOPK_COUNT  // measurement builds only: event counts of k_topk_ring (lg_topk_counts)
 __device__ unsigned long long g_topk_counts[16];
@@ -390,22 +413,41 @@ __device__ unsigned long long g_topk_counts[16];
 #define LG_CLK1(i, t) ((void)0)
 #endif
 
-// the k <= 32 ring kernel's shape: list capacity, fragment-ring buffers, chunks a wave issues
-// ahead, chunks between a piece's issue and its arrival signal (measurement builds may
-// override them: -DLG_RING_CAP=... etc.)
+// The ring kernel's shapes per list size (k <= 32 / <= 64 / <= 128): list capacity,
+// fragment-ring buffers, chunks a wave issues ahead, chunks between a piece's issue and its
+// arrival signal (measurement builds may override them: -DLG_RING_CAP=... etc.). LDS: lists
+// users x CAP x 6 B + NBUF x 8 KiB + 2 KiB within 160 KiB.
 #ifndef LG_RING_CAP
 #define LG_RING_CAP 56
 #endif
 #ifndef LG_RING_NBUF
-#define LG_RING_NBUF 5
+#define LG_RING_NBUF 9
 #endif
 #ifndef LG_RING_LA
-#define LG_RING_LA 3
+#define LG_RING_LA 5
 #endif
 #ifndef LG_RING_LAG
 #define LG_RING_LAG 1
 #endif
-// user groups per wave (2: 8 waves, two per SIMD; 4: 4 waves, one per SIMD)
+#ifndef LG_RING2_CAP
+#define LG_RING2_CAP 112
+#endif
+#ifndef LG_RING2_NBUF
+#define LG_RING2_NBUF 9
+#endif
+#ifndef LG_RING4_CAP
+#define LG_RING4_CAP 160
+#endif
+#ifndef LG_RING4_NBUF
+#define LG_RING4_NBUF 4
+#endif
+#ifndef LG_RING4_LA
+#define LG_RING4_LA 2
+#endif
+#ifndef LG_RING4_W  // waves (16 users each) per block at k <= 128
+#define LG_RING4_W 8
+#endif
+// user groups per wave at k <= 32 (2: 8 waves, two per SIMD; 4: 4 waves, one per SIMD)
 #ifndef LG_RING_NG
 #define LG_RING_NG 2
 #endif
@@ -419,13 +461,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
     float *__restrict__ part_val, int32_t *__restrict__ part_idx,
     const float *__restrict__ seed_val) {
-  // WAVES waves x NG groups of 16 users (the MFMA columns); a list of CAP entries per user, M
-  // per lane (entry e = 64 j + lane in slab j). The host picks CAP >= k + 16 + the tile's 16
-  // (k <= 32: 256 users and CAP 56; k <= 64: 128 users and CAP 112; k <= 128: 64 users and
-  // CAP 224 -- 112 KiB of lists in each)
+  // WAVES waves x NG groups of 16 users (the MFMA columns); a list of CAP entries per user, up
+  // to M per lane (entry e = 64 j + lane in slab j). The host picks CAP > k + 16 (k <= 32: 256
+  // users and CAP 56; k <= 64: 128 users and CAP 112; k <= 128: 128 users and CAP 160)
   static_assert(M == 1 || M == 2 || M == 4, "list slabs");
-  static_assert(CAP <= 64 * M && CAP >= 48 * M, "list capacity");
-  static_assert(!SEEDP || M == 1, "the seed pass serves k <= 32");
+  static_assert(CAP <= 64 * M && CAP > 32 * M, "list capacity");
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
   // the fragment ring: chunks of CI items (CB bytes, PPT 16-byte LDS-DMA pieces per thread)
@@ -434,12 +474,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   constexpr int PPT = CB / 16 / (64 * WAVES);
   static_assert(PPT >= 1 && CI * PR == 64 * WAVES * PPT, "whole DMA pieces per thread");
   static_assert(LAG >= 1 && LA > LAG && NBUF > LA, "ring shape");
-  // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane)
+  // seed classes: 16 x the tiles per ring chunk (at most 4 of them: one class per lane); the
+  // seed pass keeps the R largest lower bounds of each class (R = 4 for k > 32)
   constexpr int TPC_S = TPC < 4 ? TPC : 4;
   constexpr int NCLS = 16 * TPC_S;
-  // (the seed pass keeps its class maxima in ls instead of lists: no ids)
-  __shared__ float ls[WAVES][NG][16][SEEDP ? NCLS : CAP];
-  __shared__ uint32_t li[WAVES][NG][16][SEEDP ? 1 : CAP];
+  constexpr int R = M == 1 ? 1 : 4;
+  // the lists: keys and tile indices (6-byte entries, above)
+  __shared__ uint32_t lk[WAVES][NG][16][SEEDP ? 1 : CAP];
+  __shared__ uint16_t lt[WAVES][NG][16][SEEDP ? 1 : CAP];
   __shared__ int exs[WAVES][64];  // exclusion runs; the exact chain's results
   __shared__ __attribute__((aligned(16))) char frs[NBUF][CI * RB];
   __shared__ uint32_t prog[WAVES];  // the fragment ring's progress words (below)
@@ -576,8 +618,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     int64_t pos = __shfl(gget(ex_pos, g), u);
     const int64_t hi = __shfl(gget(ex_hi, g), u);
     const float m = __shfl(gget(marg, g), u), st = __shfl(gget(sthr, g), u);
-    float *ks = &ls[wave][g][u][0];
-    uint32_t *is = &li[wave][g][u][0];
+    uint32_t *ks = &lk[wave][g][u][0];
+    uint16_t *ts = &lt[wave][g][u][0];
     if (n > c0) {
       while (pos < hi) {
         const int64_t e = pos + lane;
@@ -590,18 +632,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
         for (int j = 0; j < M; ++j) {
           const int ej = 64 * j + lane;
-          if (ej >= c0 && ej < n) {
-            const int item = (int)is[ej];  // (entries since the last compaction: not final)
-            int a = 0, b = nin;            // first index with exs[] >= item
+          if (ej >= c0 && ej < n) {  // (entries since the last compaction: bound entries)
+            const uint32_t kbits = ks[ej];
+            const int item = (int)i0 + ((int)ts[ej] << 4) + (int)(kbits & kRowMask);
+            int a = 0, b = nin;  // first index with exs[] >= item
             while (a < b) {
               const int mid = (a + b) >> 1;
               if (exs[wave][mid] < item) a = mid + 1;
               else b = mid;
             }
-            if (a < nin && exs[wave][a] == item) {
-              ks[ej] = mask_value;
-              is[ej] = (uint32_t)item | kFinal;
-            }
+            if (a < nin && exs[wave][a] == item)
+              ks[ej] = key_pack(mask_value, (kbits & kRowMask) | kExact | kExcl);
           }
         }
         wave_sync();
@@ -609,20 +650,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         if (nin < 64) break;
       }
     }
-    bool have[M], isfin[M], keep[M];
-    float key[M], lb[M], hb[M];
-    uint32_t idr[M];
+    bool have[M], excl[M], keep[M];
+    float lb[M], hb[M];
+    uint32_t kbits[M];
+    uint16_t tix[M];
     int item[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       const int ej = 64 * j + lane;
       have[j] = ej < n;
-      key[j] = have[j] ? ks[ej] : 0.f;
-      idr[j] = have[j] ? is[ej] : 0u;
-      isfin[j] = (idr[j] & kFinal) != 0;
-      item[j] = (int)(idr[j] & ~kFinal);
-      lb[j] = isfin[j] ? key[j] : lbound(key[j], m);
-      hb[j] = isfin[j] ? key[j] : ubound(key[j], m);
+      kbits[j] = have[j] ? ks[ej] : 0u;
+      tix[j] = have[j] ? ts[ej] : (uint16_t)0;
+      excl[j] = (kbits[j] & kExcl) != 0;
+      item[j] = (int)i0 + ((int)tix[j] << 4) + (int)(kbits[j] & kRowMask);
+      const float v = key_value(kbits[j]), mj = (kbits[j] & kExact) ? 0.f : m;
+      lb[j] = excl[j] ? mask_value : lbound_t(v, mj);
+      hb[j] = excl[j] ? mask_value : ubound_t(v, mj);
       lb[j] = lb[j] == lb[j] ? lb[j] : neg_inf<float>();       // (NaN: no lower bound)
       hb[j] = hb[j] == hb[j] ? hb[j] : __builtin_huge_valf();  // (NaN: no upper bound)
     }
@@ -652,10 +695,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     }
     wave_sync();  // (every lane has read its entries)
     LG_COUNT(2, fin ? 0 : 1);
-    LG_COUNT(3, (!fin && nk > CAP - 16) ? 1 : 0);
+    // (measurement builds may make lists exact earlier: -DLG_RING_ESC=n escapes at > n entries)
+#ifdef LG_RING_ESC
+    const int esc = LG_RING_ESC < CAP - 16 ? LG_RING_ESC : CAP - 16;
+#else
+    constexpr int esc = CAP - 16;
+#endif
+    LG_COUNT(3, (!fin && nk > esc) ? 1 : 0);
     LG_COUNT(5, fin ? nk : 0);
     LG_COUNT(6, fin ? 1 : 0);
-    if (fin || nk > CAP - 16) {
+    if (fin || nk > esc) {
       float kk[M];
       int ii[M];
       int nok = 0;
@@ -663,7 +712,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       for (int j = 0; j < M; ++j) {
         const float raw = kb[j] ? exact_entries(ubase + g * 16 + u, kb[j], item[j]) : 0.f;
         const bool ok = keep[j] && raw == raw && raw > neg_inf<float>();
-        kk[j] = ok ? (isfin[j] ? key[j] : raw) : neg_inf<float>();
+        kk[j] = ok ? (excl[j] ? mask_value : raw) : neg_inf<float>();
         ii[j] = ok ? item[j] : kPadId;
         nok += __popcll(__ballot(ok));
       }
@@ -673,9 +722,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         const int ej = 64 * j + lane;
-        if (ej < nk) {
-          ks[ej] = kk[j];
-          is[ej] = (uint32_t)ii[j] | kFinal;
+        if (ej < nk) {  // (an exact score equal to the mask value may pass as excluded: the same)
+          const int rel = ii[j] - (int)i0;
+          ks[ej] = key_pack(kk[j], (uint32_t)(rel & 15) | kExact | (kk[j] == mask_value ? kExcl : 0u));
+          ts[ej] = (uint16_t)(rel >> 4);
         }
         if (nk == k && j == ((k - 1) >> 6)) tau = __shfl(kk[j], (k - 1) & 63);  // (uniform)
         ov[j] = ej < nk ? kk[j] : neg_inf<float>();
@@ -687,8 +737,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       for (int j = 0; j < M; ++j) {
         if (keep[j]) {
           const int p = base + __popcll(kb[j] & lanemask_lt());
-          ks[p] = key[j];
-          is[p] = idr[j];
+          ks[p] = kbits[j];
+          ts[p] = tix[j];
         }
         base += __popcll(kb[j]);
       }
@@ -743,8 +793,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       if (bal) {
         const int pos = cnt[g] + __popcll(bal & same_user & lanemask_lt());
         if (cand) {
-          ls[wave][g][ul][pos] = acc[r];
-          li[wave][g][ul][pos] = (uint32_t)((int)i0 + rel + r);
+          lk[wave][g][ul][pos] = key_pack(acc[r], (uint32_t)(4 * gq + r));
+          lt[wave][g][ul][pos] = (uint16_t)t;
         }
         cnt[g] += __popcll(bal & same_user);
       }
@@ -753,13 +803,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 
   const int lim_end = (int)i1;
   // the seed pass's class maxima (SEEDP only)
-  f32x4 cmax[NG][SEEDP ? TPC_S : 1];
+  f32x4 cmax[NG][SEEDP ? TPC_S : 1][SEEDP ? R : 1];  // (per class, descending)
 #pragma unroll
   for (int g = 0; g < NG; ++g)
 #pragma unroll
     for (int tt = 0; tt < (SEEDP ? TPC_S : 1); ++tt)
-      cmax[g][tt] = f32x4{neg_inf<float>(), neg_inf<float>(), neg_inf<float>(),
-                          neg_inf<float>()};
+#pragma unroll
+      for (int l = 0; l < (SEEDP ? R : 1); ++l)
+        cmax[g][tt][l] = f32x4{neg_inf<float>(), neg_inf<float>(), neg_inf<float>(),
+                               neg_inf<float>()};
   {
     // The block's waves share the bf16 item fragments through LDS: chunks of CI items (CB
     // bytes, PPT 16-byte LDS-DMA pieces per thread: global_load_lds_dwordx4, no VGPRs) in a
@@ -885,8 +937,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       }
       return gm;
     };
-    // the seed pass: each lane's running maxima of the lower bounds (past the range: -inf; a
-    // NaN stays NaN and seeds nothing), class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r
+    // the seed pass: each lane's R largest lower bounds per class (past the range: -inf),
+    // class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r; a value enters the class's sorted
+    // R slots by a max / min chain (finite margins and embeddings: the caller's contract)
     auto seed_chunk = [&](int c, const Accs &acc) __attribute__((always_inline)) {
       const int t0 = c * TPC;
 #pragma unroll
@@ -896,9 +949,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         for (int g = 0; g < NG; ++g)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float lb = rel + r < n_valid ? lbound(acc[tt][g][r], marg[g])
-                                               : neg_inf<float>();
-            cmax[g][tt % TPC_S][r] = __builtin_elementwise_maximum(cmax[g][tt % TPC_S][r], lb);
+            float v = rel + r < n_valid ? lbound(acc[tt][g][r], marg[g]) : neg_inf<float>();
+#pragma unroll
+            for (int l = 0; l < R; ++l) {
+              const float h = cmax[g][tt % TPC_S][l][r];
+              cmax[g][tt % TPC_S][l][r] = fmaxf(h, v);
+              if (l + 1 < R) v = fminf(h, v);
+            }
           }
       }
     };
@@ -1009,43 +1066,47 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 
   wave_sync();
   if constexpr (SEEDP) {
-    // per user: the (k + E)-th largest of its NCLS class maxima (E = its excluded items in this
-    // split's range, by two binary searches of its sorted exclusion row), into the K-th slot of
-    // its output row; -inf when k + E > NCLS
+    // per user: the (k + E)-th largest of its NCLS x R candidates -- distinct items' lower
+    // bounds -- (E = its excluded items in this split's range, by two binary searches of its
+    // sorted exclusion row), into the K-th slot of its output row; -inf when k + E > NCLS R.
+    // All 16 users of a group at once: a radix select whose counts sum each lane's candidates
+    // over the user's 4 lanes (gq) by two xor shuffles.
+    constexpr int NV = TPC_S * R * 4;  // candidates per lane
 #pragma unroll
-    for (int g = 0; g < NG; ++g)
+    for (int g = 0; g < NG; ++g) {
+      const int64_t user = ubase + g * 16 + ul;
+      int E = 0;
+      if (ex_rowptr && user < n_users) {
+        const int64_t e0 = ex_rowptr[user], e1 = ex_rowptr[user + 1];
+        E = (int)(lower_bound_i32(ex_col, e0, e1, (int32_t)i1) -
+                  lower_bound_i32(ex_col, e0, e1, (int32_t)i0));
+      }
+      const int need = k + E;
+      uint32_t o[NV];
 #pragma unroll
       for (int tt = 0; tt < TPC_S; ++tt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ls[wave][g][ul][16 * tt + 4 * gq + r] = cmax[g][tt][r];
-    wave_sync();
+        for (int l = 0; l < R; ++l)
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      for (int u = 0; u < 16; ++u) {
-        const int64_t user = ubase + g * 16 + u;
-        if (user >= n_users) break;
-        int E = 0;
-        if (ex_rowptr) {
-          const int64_t e0 = ex_rowptr[user], e1 = ex_rowptr[user + 1];
-          E = (int)(lower_bound_i32(ex_col, e0, e1, (int32_t)i1) -
-                    lower_bound_i32(ex_col, e0, e1, (int32_t)i0));
-        }
-        const int need = k + E;  // (wave-uniform)
-        float sv = neg_inf<float>();
-        if (need <= NCLS) {
-          const float v = lane < NCLS ? ls[wave][g][u][lane] : neg_inf<float>();
-          int rank = 0;  // entries above v, ties by class index
-          for (int j = 0; j < NCLS; ++j) {
-            const float w = ls[wave][g][u][j];
-            rank += (w > v || (w == v && j < lane)) ? 1 : 0;
+          for (int r = 0; r < 4; ++r) {
+            const float x = cmax[g][tt][l][r];
+            o[(tt * R + l) * 4 + r] = ford(x);
           }
-          const uint64_t b = __ballot(lane < NCLS && rank == need - 1);
-          if (b) sv = __shfl(v, __ffsll((long long)b) - 1);
-        }
-        if (lane == 0) {
-          if (n_splits == 1) out_val[user * k + k - 1] = sv;
-          else part_val[((int64_t)split * n_users + user) * k + k - 1] = sv;
-        }
+      uint32_t T = 0u;  // the greatest T with `need` candidates at or above it
+#pragma unroll 1
+      for (int b = 31; b >= 0; --b) {
+        const uint32_t c = T | (1u << b);
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) n += o[j] >= c ? 1 : 0;
+        n += __shfl_xor(n, 16);
+        n += __shfl_xor(n, 32);
+        if (n >= need) T = c;
+      }
+      const float sv = need <= NCLS * R ? funord(T) : neg_inf<float>();
+      if (gq == 0 && user < n_users) {
+        if (n_splits == 1) out_val[user * k + k - 1] = sv;
+        else part_val[((int64_t)split * n_users + user) * k + k - 1] = sv;
       }
     }
     return;
@@ -1279,22 +1340,30 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
                                  float *part_val, int32_t *part_idx, const float *seed_val,
                                  hipStream_t stream) {
-  // one block per CU: 112 KiB of lists + the fragment ring. k <= 32: 256 users of CAP
-  // LG_RING_CAP; k <= 64: 128 users (8 waves x 1 group) of CAP 112; k <= 128: 64 users (4 waves
-  // x 1 group) of CAP 224
-#define LG_RING_LAUNCH(NG, W, MM, CAP, SEEDP)                                                 \
+  // one block per CU: the lists (6-byte entries) + the fragment ring. k <= 32: 256 users of
+  // CAP 56 (84 KiB) + 9 ring buffers; k <= 64: 128 users (8 waves x 1 group) of CAP 112
+  // (84 KiB) + 9 buffers; k <= 128: 128 users of CAP 160 (120 KiB) + 4 buffers
+#define LG_RING_LAUNCH(NG, W, MM, CAP, NBUF, LA, SEEDP)                                       \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_topk_ring<D, NG, W, MM, CAP, LG_RING_NBUF, LG_RING_LA, LG_RING_LAG, SEEDP>              \
+    k_topk_ring<D, NG, W, MM, CAP, NBUF, LA, LG_RING_LAG, SEEDP>                              \
         <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
-  if (M == 1 && seedp) LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, true)
-  else if (M == 1) LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, false)
-  else if (M == 2) LG_RING_LAUNCH(1, 8, 2, 112, false)
-  else LG_RING_LAUNCH(1, 4, 4, 224, false)
+  if (M == 1 && seedp)
+    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, true)
+  else if (M == 1)
+    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, false)
+  else if (M == 2 && seedp)
+    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, true)
+  else if (M == 2)
+    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, false)
+  else if (seedp)
+    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, true)
+  else
+    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, false)
 #undef LG_RING_LAUNCH
 }
 
@@ -1306,14 +1375,22 @@ static int64_t split_len(int64_t n_items, int n_splits) {
   return per < 16 ? 16 : per;
 }
 
+// the screened kernel's splits: at least one per 2^20 items (k_topk_ring's 16-bit tile
+// indices); split_len of it is then <= 2^20 (a multiple of 16)
+static int screened_splits(int64_t n_items, int n_splits) {
+  const int64_t need = (n_items + ((int64_t)1 << (kTileBits + 4)) - 1) >> (kTileBits + 4);
+  return n_splits > need ? n_splits : (int)need;
+}
+
 }  // namespace lg
 
 using namespace lg;
 
 extern "C" size_t lg_score_topk_ws_bytes(int64_t n_users, int64_t n_items, int32_t dim,
                                          int32_t k, int32_t n_splits) {
-  (void)n_items;
   (void)dim;
+  // (either kernel: the screened one splits catalogs of more than 2^20 items at least)
+  if (n_items > 0 && n_splits >= 1) n_splits = screened_splits(n_items, n_splits);
   if (n_splits <= 1 || n_users <= 0 || k <= 0) return 0;
   return (size_t)n_splits * (size_t)n_users * (size_t)k * (sizeof(float) + sizeof(int32_t));
 }
@@ -1386,7 +1463,8 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
   LG_REQUIRE(((uintptr_t)eu_bf16 & 15) == 0 && ((uintptr_t)ei_bf16 & 15) == 0,
              "lg_score_topk_screened_f32: bf16 copies must be 16-byte aligned");
   if (n_users == 0) return LG_OK;
-  const int64_t per = split_len(n_items, n_splits);
+  // (the lists' 16-bit tile indices: splits of at most 2^20 items)
+  const int64_t per = split_len(n_items, screened_splits(n_items, n_splits));
   const int ns = (int)((n_items + per - 1) / per);
   float *part_val = nullptr;
   int32_t *part_idx = nullptr;
@@ -1424,13 +1502,13 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
                                                           out_val, out_idx);
     return launch_status("lg_score_topk_screened_f32(merge)");
   };
-  // the seed pass (k <= 32, large catalogs): the screen-only lower-bound class maxima over the
-  // first 1/16 of the items, each user's seed into the K-th slot of its out_val row (the main
+  // the seed pass (large catalogs): the screen-only lower-bound class maxima (the R largest per
+  // class for k > 32) over the first 1/16 of the items, each user's seed into the K-th slot of its out_val row (the main
   // pass reads it there before it writes anything: a user's seed and its list belong to the
   // same wave), on at most as many splits as the main pass (their seeds fit the same
   // workspace; the largest is kept)
   const int64_t n_seed = n_items / LG_TOPK_SEED_DIV / 16 * 16;
-  const bool seeded = M == 1 && lg_topk_seeding() && n_seed >= (int64_t)k * 64;
+  const bool seeded = lg_topk_seeding() && n_seed >= (int64_t)k * 64;
   if (seeded) {
     const int64_t per_s = split_len(n_seed, ns);
     const int ns_s = (int)((n_seed + per_s - 1) / per_s);

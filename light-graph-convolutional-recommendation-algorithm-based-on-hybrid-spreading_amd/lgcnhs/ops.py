@@ -170,7 +170,7 @@ def propagate(adj: Adjacency, e0: torch.Tensor, layers: int) -> torch.Tensor:
 # ------------------------------------------------------------------------------ scoring
 def _resident_blocks(device, k: int = 64, screen: bool = False) -> int:
     """Workgroups resident at once: lg_score_topk_f32's take 64 KiB of LDS -> 2 per CU; the
-    screened kernel's (k_topk_ring: 112 KiB of lists + the fragment ring) -> 1 per CU."""
+    screened kernel's (k_topk_ring: 84-120 KiB of lists + the fragment ring) -> 1 per CU."""
     per_cu = 1 if screen else 2
     return per_cu * torch.cuda.get_device_properties(device).multi_processor_count
 
@@ -178,7 +178,7 @@ def _resident_blocks(device, k: int = 64, screen: bool = False) -> int:
 def _users_per_block(k: int, screen: bool = False) -> int:
     """Users per workgroup of csrc/topk.hip's launches (dispatch_topk / _screen)."""
     if screen:
-        return 256 if k <= 32 else (128 if k <= 64 else 64)
+        return 256 if k <= 32 else 128
     return 128 if k <= 32 else (64 if k <= 64 else 32)
 
 

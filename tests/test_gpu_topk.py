@@ -115,16 +115,18 @@ def test_screened_topk_non_finite_rows(I):
     assert (i[np.arange(U) != 7] >= 0).all() and not (i == 1234).any()
 
 
-@pytest.mark.parametrize("k", [1, 20, 32])
+@pytest.mark.parametrize("k", [1, 20, 32, 64, 100])
 def test_seeded_topk_exclusions_in_seed_range(k):
-    """The screened kernel's seed pass (k <= 32, catalogs of >= 1024 k items): every user's
-    threshold starts at the (k + E)-th largest class maximum of the lower bounds over the first
-    1/16 of the items, E = its excluded items there. Users whose best items of that range are
-    excluded (E from 0 to 60: the seed must skip them, and there is none once k + E > 64), items
-    tied in bf16 and exactly inside the range, a zero user, users scaled over 1e-2..1e2: the
-    lists equal the plain kernel's and the C oracle's bit for bit."""
+    """The screened kernel's seed pass (catalogs of >= 1024 k items): every user's threshold
+    starts at the (k + E)-th largest of the lower bounds kept per item class over the first
+    1/16 of the items (the class maximum for k <= 32, the 4 largest per class above), E = its
+    excluded items there. Users whose best items of that range are excluded (E from 0 to 60:
+    the seed must skip them, and there is none once k + E exceeds the candidates), items tied
+    in bf16 and exactly inside the range, a zero user, users scaled over 1e-2..1e2: the lists
+    equal the plain kernel's and the C oracle's bit for bit."""
     from lgcnhs import ops
-    U, I, d = 200, 65536, 64
+    U, d = 200, 64
+    I = 65536 if k <= 64 else 131072
     eu, ei = _emb(U, d, 51 + k), _emb(I, d, 52)
     ei[100:140] = ei[60:100]  # exact ties inside the seed range
     g = torch.Generator().manual_seed(53)
