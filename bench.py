@@ -738,12 +738,14 @@ def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):
 def topk_roofline(nu, I, D, k, tk):
     """roofline of the screened top-K (MFMA-bound): the MFMA work it executes priced against
     the dense bf16 peak (k_topk_ring, bound-side lists, every k): the bf16 screen of every
-    (user, item), plus for k <= 32 the seed pass's screen of the first 1/16 of the items
-    (catalogs of >= 1024 k items); the exact fp32 chains run only on the surviving entries per
-    user (~k + 9 at k = 20) and are counted from the PMC record (f32 MFMAs beyond the screen's)
+    (user, item), plus the seed pass's screen of the first 1/16 of the items (catalogs of
+    >= 1024 k items); the exact fp32 chains run only on the surviving entries per user
+    (~k + 9 at k = 20) and are counted from the PMC record (f32 MFMAs beyond the screen's)
     at the bf16 / fp32 peak ratio. The record (profiles/pmc_topk.json,
     scripts/gpu_topk_pmc.sh + scripts/topk_pmc_summary.py) is used only if taken on this
-    csrc/topk.hip at this shape; it also gives the PMC MFMA-busy fraction and HBM traffic."""
+    csrc/topk.hip at this shape (users per rank, items, k); it also gives the PMC MFMA-busy
+    fraction and HBM traffic. Without one (e.g. the N > 1 lines' per-rank user blocks) the
+    frac counts the screen alone and says so in frac_basis."""
     import hashlib
     sha = hashlib.sha256(open(os.path.join(PKG, "csrc", "topk.hip"), "rb").read()).hexdigest()[:16]
     key = f"c5-d{D}/topk" + ("" if k == 20 else f"_k{k}")
@@ -752,23 +754,30 @@ def topk_roofline(nu, I, D, k, tk):
         rec = json.load(open(os.path.join(REPO, "profiles", "pmc_topk.json"))).get(key)
     except Exception:
         rec = None
+    scale = 1.0  # the record's exact chains per launch -> this launch's
     if rec is not None:
         if rec.get("kernel_sha") != sha:
             rec, status = None, "stale: recorded on another topk.hip"
-        elif (rec.get("users"), rec.get("items"), rec.get("k")) != (nu, I, k):
+        elif (rec.get("items"), rec.get("k")) != (I, k):
             rec, status = None, "recorded at another shape"
+        elif rec.get("users") != nu:
+            # another user block of the same catalog and k (the N > 1 lines' per-rank share):
+            # the exact chains per user are a property of the workload, scaled by users
+            scale, status = nu / rec["users"], "measured at N = 1, scaled per user"
         else:
             status = "measured"
-    seeded = k <= 32 and I // 16 // 16 * 16 >= 64 * k
+    seeded = I // 16 // 16 * 16 >= 64 * k
     bf16 = 2.0 * nu * I * D * (1.0 + (1.0 / 16 if seeded else 0.0))
     # fp32 MFMA flops of the exact chains: 16x16x4 f32 MFMA = 2048 flop each
-    f32 = 2048.0 * rec["f32_mfma_per_launch"] if rec else 0.0
+    f32 = 2048.0 * rec["f32_mfma_per_launch"] * scale if rec else 0.0
     achieved = (bf16 + f32 * BF16_MFMA_PEAK_TF / F32_MFMA_PEAK_TF) / tk / 1e12
     return {"bound": "mfma", "achieved": achieved, "peak": BF16_MFMA_PEAK_TF,
             "unit": "TFLOP/s (bf16-equivalent MFMA work)", "frac": achieved / BF16_MFMA_PEAK_TF,
             "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
             "kernel": "lg_score_topk_screened_f32", "avg_launch_ms": tk * 1e3,
-            "exact_f32_mfma_per_launch": rec.get("f32_mfma_per_launch") if rec else None,
+            "frac_basis": ("bf16 screen + seed pass + the exact chains" if rec else
+                           "bf16 screen + seed pass only (no exact-chain record for this shape)"),
+            "exact_f32_mfma_per_launch": rec["f32_mfma_per_launch"] * scale if rec else None,
             "pmc_mfma_busy_frac": rec.get("mfma_busy_frac") if rec else None,
             "pmc_avg_ms": rec.get("avg_ms") if rec else None,
             "pmc_wave_parked_frac": rec.get("wave_parked_frac") if rec else None,
@@ -779,8 +788,8 @@ def topk_roofline(nu, I, D, k, tk):
 def load_traffic(workload, world, src_name="spmm.hip", key=None):
     """roofline.traffic: HBM bytes per launch of a kernel from the PMC pass recorded in
     profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH x 2 per the
-    gfx950 correction; K1: scripts/profile.sh + scripts/pmc_summary.py under
-    "<workload>/n<world>", the K3s walk: scripts/gpu_r02_walk_traffic.sh +
+    gfx950 correction; K1: scripts/gpu_traffic.sh + scripts/pmc_summary.py under
+    "<workload>/n<world>", the K3s walk: scripts/gpu_traffic.sh +
     scripts/walk_traffic_summary.py under "c5-d64/spread_walk"). The entry is used only if
     the kernel source it was measured on (sha256 of csrc/<src_name>) is the one built now;
     otherwise traffic is null and the reason is reported."""
@@ -916,6 +925,8 @@ def main():
     ap.add_argument("--workload", default="c5-d64", choices=sorted(WORKLOADS))
     ap.add_argument("--topk-users", type=int, default=32768, help="users per rank for the top-K phase")
     ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--k-long", type=int, default=100,
+                    help="the topk_k100 leg's list length (0: no leg)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-topk", action="store_true")
     ap.add_argument("--no-spread", action="store_true")
@@ -1081,6 +1092,14 @@ def main():
     if not args.no_topk:
         topk, topk_gpu_lists = bench_topk(e0_orig, keys, U, I, D, args.k, args.topk_users,
                                           rank, world, dev)
+    # the reference's production list length (const.py:433, k = 100) on the same users
+    topk_k100 = topk_k100_lists = None
+    if not args.no_topk and args.k_long and args.k_long != args.k:
+        try:
+            topk_k100, topk_k100_lists = bench_topk(e0_orig, keys, U, I, D, args.k_long,
+                                                    args.topk_users, rank, world, dev)
+        except Exception as ex:  # a side measurement never hides the main result
+            log(f"k={args.k_long} topk bench failed: {ex!r}")
 
     spread = None
     if not args.no_spread:
@@ -1106,6 +1125,10 @@ def main():
                 n_cmp = min(cpu_lists.shape[0], topk_gpu_lists.shape[0])
                 topk["parity_vs_cpu_reference"] = topk_parity(
                     topk_gpu_lists[:n_cmp], cpu_lists[:n_cmp], e0_orig, U, D, args.k)
+            if topk_k100 is not None and topk_k100_lists is not None:
+                _, cpu_l100 = cpu_baseline_topk(e0_orig, keys, U, I, args.k_long, n_users=1024)
+                topk_k100["parity_vs_cpu_reference"] = topk_parity(
+                    topk_k100_lists[:1024], cpu_l100, e0_orig, U, D, args.k_long)
             cpu_spread = cpu_baseline_spread(args.k)
         except Exception as ex:  # the baseline must never hide the GPU result
             log(f"cpu baseline failed: {ex!r}")
@@ -1134,6 +1157,7 @@ def main():
                          "job_frac": value / (world * HBM_PEAK_GBS * 1e9 * nnz / job_bytes)},
             "comm": comm,
             "topk": topk,
+            "topk_k100": topk_k100,
             "spread": spread,
             "train": train,
             "other_dims": extra,

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 kernel-trace + PMC passes (scripts/profile.sh output) into
+"""Summarise rocprofv3 kernel-trace + PMC passes (scripts/gpu_traffic.sh output) into
 profiles/: per-kernel average duration, FETCH_SIZE / WRITE_SIZE per launch and the HBM
 traffic estimate bench.py reports as roofline.traffic.
 
@@ -22,13 +22,16 @@ def kernel_key(name):
     return None
 
 
-def main(out_dir, tag, workload="c5-d64", world=1):
+def main(out_dir, tag, workload="c5-d64", world=1, g=None):
     """Per kernel, the launch shape (grid size) with the most total time is the headline
     launch (the bench also runs side configurations); every statistic below is over the
-    dispatches of that shape only."""
-    g = os.path.join(REPO, "gpurun_out")
+    dispatches of that shape only. g: the passes' directory, holding trace/ fetch/ write/
+    (scripts/gpu_traffic.sh: gpurun_out/<out>/k1_<workload>) or prof_trace/ prof_fetch/
+    prof_write/ (scripts/profile.sh: gpurun_out)."""
+    g = g or os.path.join(REPO, "gpurun_out")
+    pre = "prof_" if os.path.isdir(os.path.join(g, "prof_trace")) else ""
     groups = defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(g, "prof_trace", "run_kernel_trace.csv"))):
+    for r in csv.DictReader(open(os.path.join(g, pre + "trace", "run_kernel_trace.csv"))):
         k = kernel_key(r["Kernel_Name"])
         if k:
             groups[(k, int(r["Grid_Size_X"]))].append(
@@ -43,8 +46,8 @@ def main(out_dir, tag, workload="c5-d64", world=1):
         stats[k] = {"grid_size": grid, "calls": len(d), "avg_ms": sum(d) / len(d),
                     "min_ms": d[0], "max_ms": d[-1]}
     ctr = defaultdict(list)
-    for sub in ("prof_fetch", "prof_write", "prof_sq"):
-        path = os.path.join(g, sub, "run_counter_collection.csv")
+    for sub in ("fetch", "write", "sq"):
+        path = os.path.join(g, pre + sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
         for r in csv.DictReader(open(path)):
@@ -65,7 +68,6 @@ def main(out_dir, tag, workload="c5-d64", world=1):
             s["hbm_bytes_per_launch"] = (2 * s["FETCH_SIZE_KiB_per_launch"]
                                          + s["WRITE_SIZE_KiB_per_launch"]) * 1024
     os.makedirs(out_dir, exist_ok=True)
-    json.dump(stats, open(os.path.join(out_dir, f"{tag}_kernel_summary.json"), "w"), indent=1)
     tp = os.path.join(out_dir, "pmc_traffic.json")
     d = json.load(open(tp)) if os.path.exists(tp) else {}
     if "lg_spmm_layer_f32" in stats and "hbm_bytes_per_launch" in stats["lg_spmm_layer_f32"]:
@@ -80,6 +82,7 @@ def main(out_dir, tag, workload="c5-d64", world=1):
 
 
 if __name__ == "__main__":
-    # usage: pmc_summary.py TAG [WORKLOAD (c5-d64)]
-    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r02",
-         sys.argv[2] if len(sys.argv) > 2 else "c5-d64")
+    # usage: pmc_summary.py TAG [WORKLOAD (c5-d64)] [DIR]
+    main(os.path.join(REPO, "profiles"), sys.argv[1] if len(sys.argv) > 1 else "r05",
+         sys.argv[2] if len(sys.argv) > 2 else "c5-d64",
+         g=sys.argv[3] if len(sys.argv) > 3 else None)

@@ -1,5 +1,5 @@
 """Per-launch HBM traffic of the fused K3s walk (k_tile_walk, lg_spread_tile_resource_topk_f64)
-from scripts/gpu_r02_walk_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE (the gfx950 corrections of
+from scripts/gpu_traffic.sh (walk_d<D>/): FETCH_SIZE x 2 + WRITE_SIZE (the gfx950 corrections of
 MI355X_MICROARCH.md, as scripts/pmc_summary.py for K1), averaged over the launches after the
 first tile (whose list fill makes it atypical), recorded in profiles/pmc_traffic.json under
 "<workload>/spread_walk" with the hash of csrc/spread_tiled.hip (bench.py uses it only for that

@@ -56,10 +56,12 @@ def test_world_size_must_match_gpus():
 
 
 def test_topk_roofline_prices_the_screen_the_seed_pass_and_the_exact_chains():
-    """bench.topk_roofline: bf16 work = the screen of every (user, item) plus, for k <= 32 on a
-    large catalog, the seed pass's screen of the first 1/16 of the items; the fp32 exact chains
-    (k <= 32: the f32 MFMAs of the final ranking, from the PMC record of this topk.hip,
-    profiles/pmc_topk.json) priced at the bf16 / fp32 MFMA peak ratio."""
+    """bench.topk_roofline: bf16 work = the screen of every (user, item) plus, on a large
+    catalog, the seed pass's screen of the first 1/16 of the items; the fp32 exact chains (the
+    f32 MFMAs of the final ranking, from the PMC record of this topk.hip, profiles/
+    pmc_topk.json) priced at the bf16 / fp32 MFMA peak ratio; another user block of the same
+    catalog and k (an N > 1 rank's share) scales the record's chains per user; a shape without
+    a record counts the screen alone and says so in frac_basis."""
     sys.path.insert(0, REPO)
     import bench
     nu, I, D, t = 32768, 1_000_000, 64, 0.0105
@@ -68,15 +70,20 @@ def test_topk_roofline_prices_the_screen_the_seed_pass_and_the_exact_chains():
     f32 = r["exact_f32_mfma_per_launch"]
     if r["record_source"]["status"] == "measured":
         assert f32 is not None and 0 <= 2048.0 * f32 < 0.01 * base  # (~29 chains per user)
+        assert "exact chains" in r["frac_basis"] and "only" not in r["frac_basis"]
+        # a rank's quarter of the users: the same chains per user
+        r4 = bench.topk_roofline(nu // 4, I, D, 20, t)
+        assert r4["record_source"]["status"].startswith("measured at N = 1")
+        assert abs(r4["exact_f32_mfma_per_launch"] - f32 / 4) < 1e-6 * f32
     want = (base * (1 + 1 / 16) + 2048.0 * (f32 or 0.0) * bench.BF16_MFMA_PEAK_TF /
             bench.F32_MFMA_PEAK_TF) / t / 1e12
     assert abs(r["achieved"] - want) < 1e-9 * want
     assert abs(r["frac"] - want / bench.BF16_MFMA_PEAK_TF) < 1e-12
-    # k > 32: no seed pass; a shape without a record: the screen alone, flagged
+    # a shape without a record (k = 33): the screen and the seed pass alone, flagged
     r2 = bench.topk_roofline(nu, I, D, 33, t)
     assert r2["exact_f32_mfma_per_launch"] is None
-    assert r2["record_source"]["status"] != "measured"
-    assert abs(r2["achieved"] - base / t / 1e12) < 1e-9 * r2["achieved"]
+    assert r2["record_source"]["status"] != "measured" and "only" in r2["frac_basis"]
+    assert abs(r2["achieved"] - base * (1 + 1 / 16) / t / 1e12) < 1e-9 * r2["achieved"]
 
 
 def test_gpus_2_line_carries_the_exchange_exposure():

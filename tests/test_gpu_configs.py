@@ -160,13 +160,15 @@ def test_c5_forward_sampled_rows_d128(c5):
         np.testing.assert_allclose(got[t], acc / 4, rtol=0, atol=TOL)
 
 
-def test_c5_top20_512_users_vs_reference_ops(c5):
-    """lg_score_topk_f32 over all 1M items for 512 users (train|val = every interaction
-    masked) against torch.matmul + -1024 index-put + torch.topk on the host."""
+@pytest.mark.parametrize("k", [20, 100])
+def test_c5_topk_512_users_vs_reference_ops(c5, k):
+    """The screened top-K (the product default) over all 1M items for 512 users (train|val =
+    every interaction masked) against torch.matmul + -1024 index-put + torch.topk on the
+    host, at k = 20 and at the reference's production k = 100 (const.py:433)."""
     from lgcnhs import ops
     from lgcnhs.graph import RowSets
     U, I, _, _, keys, e0 = c5
-    nu, k = 512, 20
+    nu = 512
     eu, ei = e0[:nu].contiguous(), e0[U:].contiguous()
     ku = keys[keys < nu * I]
     excl = RowSets.from_pairs(ku // I, ku % I, nu, I, DEV)
@@ -177,7 +179,7 @@ def test_c5_top20_512_users_vs_reference_ops(c5):
     ex64 = lambda u, it: ein[it].astype(np.float64) @ eun[u].astype(np.float64)  # noqa: E731
     tol = lambda u, it: _dot_tols(eun[u], ein, it, 128)  # noqa: E731
     ties, n = compare_topk_exact(got.cpu().numpy(), ref.numpy(), ex64, tol,
-                                 "C5 top-20 (512 users x 1M items)")
+                                 f"C5 top-{k} (512 users x 1M items)")
     assert ties <= max(2, n // 100)
 
 
