@@ -441,6 +441,15 @@ def test_score_bounds_cover_chain_scores_many_blocks(d):
     bad = colb < G
     assert not bad.any(), (np.argwhere(bad)[:5], colb[bad][:5], G[bad][:5])
     assert np.mean(colb - G) < np.mean(gbn[:, chunk] - G)
+    # the kernel's waits leave the chunk's own stores in flight (named counts, gbound.hip):
+    # gb alone (no q stores) and an odd chunk count (a lone last chunk) give the same gb bits
+    gb_only = ops.chunk_bounds(ub, un, ib, inn, d, j0, W)
+    assert torch.equal(gb_only.view(torch.int32), gb.view(torch.int32))
+    W3 = W - 64 * 3  # 29 chunks
+    q3 = torch.zeros((U, W), dtype=torch.uint8, device=DEV)
+    gb3, q3 = ops.chunk_bounds(ub, un, ib, inn, d, j0, W3, qout=q3)
+    assert torch.equal(gb3[:, :28].view(torch.int32), gb[:, :28].view(torch.int32))
+    assert torch.equal(q3[:, :64 * 28], q[:, :64 * 28])
 
 
 @pytest.mark.parametrize("W", [333, 300, 64, 1])
