@@ -95,6 +95,47 @@ __global__ __launch_bounds__(256) void k_bound_prep(const float *__restrict__ x,
   }
 }
 
+// The same for dim = 4 LPR (LPR = 8, 16, 32 lanes per row: dim 32, 64, 128): each lane takes
+// 4 consecutive elements (one 16-byte load, one 8-byte store), 64 / LPR rows per wave, the
+// row's sums over its LPR lanes in log2(LPR) xor steps -- the one-wave-per-row form above spent
+// its time in six fp64 shuffle steps per row (0.28 ms for a 1M x 64 table).
+template <int LPR>
+__global__ __launch_bounds__(256) void k_bound_prep4(const float *__restrict__ x, int64_t n,
+                                                     __bf16 *__restrict__ xb,
+                                                     float *__restrict__ norm,
+                                                     float *__restrict__ err) {
+  constexpr int dim = 4 * LPR, RPW = 64 / LPR;
+  const int lane = lane_id();
+  const int64_t r = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * RPW + lane / LPR;
+  const bool in = r < n;
+  const int64_t rr = in ? r : n - 1;
+  const int c = 4 * (lane % LPR);
+  const float4 v = *reinterpret_cast<const float4 *>(x + rr * dim + c);
+  const float vv[4] = {v.x, v.y, v.z, v.w};
+  double ss = 0.0, se = 0.0;
+  __bf16 b[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    b[t] = (__bf16)vv[t];
+    ss += (double)vv[t] * (double)vv[t];
+    const double e = (double)vv[t] - (double)(float)b[t];
+    se += e * e;
+  }
+  if (in) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4 *>(xb + r * dim + c) = bf16x4{b[0], b[1], b[2], b[3]};
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) {
+    ss += __shfl_xor(ss, o);
+    se += __shfl_xor(se, o);
+  }
+  if (in && lane % LPR == 0) {
+    norm[r] = round_up_f32(sqrt(ss) * (1.0 + 1e-12));
+    if (err) err[r] = round_up_f32(sqrt(se) * (1.0 + 1e-12));
+  }
+}
+
 // One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile; a block = 4
 // waves = 256 users. The chunk's item fragments (64 items x D bf16) are shared by the block's
 // waves through LDS: the 256 threads load chunk c + 1 into registers while chunk c is computed
@@ -338,8 +379,19 @@ extern "C" int lg_bound_prep_f32(const float *x, int64_t n_rows, int32_t dim, vo
   LG_REQUIRE(x && x_bf16 && norm_up && n_rows >= 0 && dim >= 1,
              "lg_bound_prep_f32: bad arguments");
   if (n_rows == 0) return LG_OK;
-  k_bound_prep<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
-      x, n_rows, dim, (__bf16 *)x_bf16, norm_up, err_up);
+  hipStream_t s = (hipStream_t)stream;
+  __bf16 *xb = (__bf16 *)x_bf16;
+  const bool al = ((uintptr_t)x & 15) == 0 && ((uintptr_t)x_bf16 & 7) == 0;
+#define LG_PREP4(LPR)                                                                         \
+  k_bound_prep4<LPR><<<dim3((unsigned)((n_rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR)))),     \
+                       dim3(256), 0, s>>>(x, n_rows, xb, norm_up, err_up)
+  if (al && dim == 32) LG_PREP4(8);
+  else if (al && dim == 64) LG_PREP4(16);
+  else if (al && dim == 128) LG_PREP4(32);
+  else
+    k_bound_prep<<<dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, s>>>(
+        x, n_rows, dim, xb, norm_up, err_up);
+#undef LG_PREP4
   return launch_status("lg_bound_prep_f32");
 }
 

@@ -209,3 +209,23 @@ def test_recommend_for_all_user_vs_reference(golden, name):
     _, oi = O.chain_topk(m.users_emb.weight.detach().cpu().numpy(),
                          m.items_emb.weight.detach().cpu().numpy(), rp, col, k)
     np.testing.assert_array_equal(got, oi)
+
+
+@pytest.mark.parametrize("d,n", [(32, 1001), (64, 4099), (128, 777), (48, 300)])
+def test_bound_prep_rounds_and_bounds(d, n):
+    """lg_bound_prep_f32 (the screen's operands): the bf16 copy is round-to-nearest-even of
+    every element (torch's conversion), and the fp32 norms ||x|| and ||x - bf16(x)|| are
+    rounded up -- >= the fp64 norms, within 1e-6 of them -- for the vectorised dims (32, 64,
+    128) and the general kernel (48), row counts that leave partial waves."""
+    from lgcnhs import ops
+    g = torch.Generator().manual_seed(d + n)
+    x = torch.randn(n, d, generator=g) * torch.exp(torch.randn(n, 1, generator=g) * 2)
+    x[3] = 0.0
+    xb, nu, ne = ops.bound_operands(x.to(DEV), with_err=True)
+    assert torch.equal(xb.cpu().view(torch.int16), x.to(torch.bfloat16).view(torch.int16))
+    x64 = x.double()
+    n64 = x64.norm(dim=1)
+    e64 = (x64 - x.to(torch.bfloat16).double()).norm(dim=1)
+    for got, ref in ((nu.cpu().double(), n64), (ne.cpu().double(), e64)):
+        assert (got >= ref).all()
+        assert ((got - ref) <= 1e-6 * ref + 1e-38).all()
