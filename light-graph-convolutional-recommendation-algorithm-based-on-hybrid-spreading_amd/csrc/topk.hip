@@ -1345,27 +1345,29 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
   // one block per CU: the lists (6-byte entries) + the fragment ring. k <= 32: 256 users of
   // CAP 56 (84 KiB) + 9 ring buffers; k <= 64: 128 users (8 waves x 1 group) of CAP 112
   // (84 KiB) + 9 buffers; k <= 128: 128 users of CAP 160 (120 KiB) + 4 buffers
-#define LG_RING_LAUNCH(NG, W, MM, CAP, NBUF, LA, SEEDP)                                       \
+#define LG_RING_LAUNCH(NG, W, MM, CAP, NBUF, LA, LAG, SEEDP)                                  \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_topk_ring<D, NG, W, MM, CAP, NBUF, LA, LG_RING_LAG, SEEDP>                              \
+    k_topk_ring<D, NG, W, MM, CAP, NBUF, LA, LAG, SEEDP>                                      \
         <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
             n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
   }
   if (M == 1 && seedp)
-    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, true)
+    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
+                   LG_RING_LAG, true)
   else if (M == 1)
-    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA, false)
+    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
+                   LG_RING_LAG, false)
   else if (M == 2 && seedp)
-    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, true)
+    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, true)
   else if (M == 2)
-    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, false)
+    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, false)
   else if (seedp)
-    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, true)
+    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true)
   else
-    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, false)
+    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false)
 #undef LG_RING_LAUNCH
 }
 
