@@ -697,11 +697,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     }
     wave_sync();  // (every lane has read its entries)
     LG_COUNT(2, fin ? 0 : 1);
-    // (measurement builds may make lists exact earlier: -DLG_RING_ESC=n escapes at > n entries)
+    // escape (make the list exact) when more entries stay than room for a tile; for the
+    // 4-slab lists (k <= 128) already at k + 30: their exact k-th value then bounds the next
+    // insertions (k = 100 at C5: 31.2 -> 28.2 ms; k + 18 / 24 / 36: 32.3 / 28.4 / 28.7 ms; the
+    // same for k <= 64 lists was slower). (Measurement builds: -DLG_RING_ESC=n escapes at > n.)
 #ifdef LG_RING_ESC
     const int esc = LG_RING_ESC < CAP - 16 ? LG_RING_ESC : CAP - 16;
 #else
-    constexpr int esc = CAP - 16;
+    const int esc = M == 4 && k + 30 < CAP - 16 ? k + 30 : CAP - 16;
 #endif
     LG_COUNT(3, (!fin && nk > esc) ? 1 : 0);
     LG_COUNT(5, fin ? nk : 0);
