@@ -452,6 +452,18 @@ __device__ unsigned long long g_topk_counts[16];
 #define LG_RING_NG 2
 #endif
 
+// the fragment ring's chunk: 8 KiB for 8 waves (64 items at d = 64), 4 or 8 KiB for 4; other
+// wave counts (measurement shapes): the smallest multiple of one 16-byte piece per thread of
+// >= 4 KiB that holds whole 16-item tiles
+constexpr int ring_chunk_bytes(int D, int W) {
+  if (W == 8 || W == 4) return D >= 64 || W >= 8 ? 8192 : 4096;
+  for (int m = 1; m < 64; ++m) {
+    const int cb = 1024 * W * m;
+    if (cb >= 4096 && (cb / (2 * D)) % 16 == 0) return cb;
+  }
+  return 0;
+}
+
 template <int D, int NG, int WAVES, int M, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
 __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
@@ -469,7 +481,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
   // the fragment ring: chunks of CI items (CB bytes, PPT 16-byte LDS-DMA pieces per thread)
-  constexpr int CB = D >= 64 || WAVES >= 8 ? 8192 : 4096;  // (>= one 16-byte piece per thread)
+  constexpr int CB = ring_chunk_bytes(D, WAVES);
   constexpr int CI = CB / (2 * D), TPC = CI / 16, PR = D / 8, RB = 2 * D;
   constexpr int PPT = CB / 16 / (64 * WAVES);
   static_assert(PPT >= 1 && CI * PR == 64 * WAVES * PPT, "whole DMA pieces per thread");
@@ -1367,10 +1379,13 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
     LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, true)
   else if (M == 2)
     LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, false)
-  else if (seedp)
-    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true)
-  else
-    LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false)
+  else if constexpr (D > 64) {  // (the LG_RING4_* shapes apply to d <= 64)
+    if (seedp) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, true)
+    else LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, false)
+  } else {
+    if (seedp) LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true)
+    else LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false)
+  }
 #undef LG_RING_LAUNCH
 }
 
