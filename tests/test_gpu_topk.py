@@ -229,3 +229,25 @@ def test_bound_prep_rounds_and_bounds(d, n):
     for got, ref in ((nu.cpu().double(), n64), (ne.cpu().double(), e64)):
         assert (got >= ref).all()
         assert ((got - ref) <= 1e-6 * ref + 1e-38).all()
+
+
+def test_screened_topk_catalog_over_2_20_items():
+    """The screened kernel's list entries hold a 16-bit tile index, so lg_score_topk_screened_f32
+    splits a catalog of more than 2^20 items (here 1,100,017: two splits even when one is asked
+    for, the workspace sized by lg_score_topk_ws_bytes for it): bit-exact vs the C oracle, with
+    a 20-user block whose best items sit past item 2^20."""
+    from lgcnhs import _native as N
+    from lgcnhs import ops
+    U, I, k = 96, 1_100_017, 20
+    assert N.lib().lg_score_topk_ws_bytes(U, I, 64, k, 1) == 2 * U * k * 8
+    eu, ei = _emb(U, 64, 61), _emb(I, 64, 62)
+    ei[(1 << 20) + 5:(1 << 20) + 25] = eu[:20] * 3.0  # user u's best item: 2^20 + 5 + u
+    rp, col = _excl(U, I, 2e-5, 63)
+    ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
+    for ns in (1, None):
+        v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), n_splits=ns,
+                              screen=True)
+        np.testing.assert_array_equal(i.cpu().numpy(), oi)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+    assert (oi[:20, 0] >= (1 << 20)).all()
+

@@ -83,6 +83,9 @@ def test_argument_validation_without_gpu():
     assert st == 1 and b"width 4097 > 4096" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
+    # catalogs of more than 2^20 items: the screened kernel's splits (16-bit tile indices)
+    assert lib.lg_score_topk_ws_bytes(100, (1 << 20) + 1, 64, 10, 1) == 2 * 100 * 10 * 8
+    assert lib.lg_score_topk_ws_bytes(100, 1 << 20, 64, 10, 1) == 0
 
 
 def test_missing_library_fails_loudly(tmp_path):
