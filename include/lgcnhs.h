@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 12
+#define LG_ABI_VERSION 13
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -231,7 +231,7 @@ int lg_rows_topk_f64(const double *F, int64_t ldf, int64_t n_rows, int64_t n_col
  *   F[u][j] = rb_j * sum over the paths u -> i -> v -> j of fl(1/k_v) * ra_i
  * (ra = 1/alpha, rb = 1/beta; each term within a few ulp of the reference's W entry, the
  * summation order the walk's own, fixed). Tiles [j0, j0 + tile) of item columns are built
- * a group of <= 8 at a time: lg_spread_group_cursor -> lg_spread_group_bound ->
+ * a group of <= 16 at a time: lg_spread_group_cursor -> lg_spread_group_bound ->
  * lg_spread_group_units -> (inclusive scan of the units) -> lg_spread_group_rows_f64; each
  * tile is then walked by lg_spread_tile_resource_topk_f64 (running top-K lists), with
  * lg_score_chunk_bound's score bounds when there is a G factor. The orchestration
@@ -263,10 +263,10 @@ int lg_inv_degree_f64(const int64_t *rowptr, int64_t n_rows, double *inv,
  * Lambda-independent (a sweep reuses the tile); line n_items (the walk's padding row) is
  * zeroed by the caller.
  *
- * Group build: n_tiles (<= 8) consecutive tiles at once, each
+ * Group build: n_tiles (<= 16; <= 8 for tiles wider than 4096) consecutive tiles at once, each
  * (item row, user) pair visited once per group instead of once per tile. Tile t of the group
  * is [group_begin + t tile, min(group_begin + (t + 1) tile, stop)).
- * lg_spread_group_cursor: counts[v][0..7] (8 uint16 per user, 16-byte aligned, unused
+ * lg_spread_group_cursor: counts[v][0..15] (16 uint16 per user, 16-byte aligned, unused
  *   tiles 0) = user v's items in each tile, end[v] = the position after the group's last
  *   (cur[v] = the first position with item >= group_begin; cur and end must not alias;
  *   positions < 2^32), rec[v] (16 bytes per user, 16-byte aligned) = the user's record for

@@ -304,16 +304,20 @@ __global__ __launch_bounds__(256) void k_hub_list(const int64_t *__restrict__ bo
 // write the group's tiles together (tile t of the group at lines + t (n_items + 1) 32 words,
 // its overflow runs at ovf + 4 ovf_base[t] words). Every word equals the per-tile build's
 // (same slot order, same headers; the caller places the runs with the same exclusive prefix).
-constexpr int kGroupMax = 8;
+constexpr int kGroupMax = 16;
+constexpr int kGroupWide = 8;  // groups of tiles wider than 4096 columns (13-bit item codes)
 
-// counts[v][t] (kGroupMax uint16 per user) = the items of user v in tile t of the group
-// ([group_begin + t tile, min(group_begin + (t + 1) tile, stop))), end[v] = the position
-// after the group's last; cur[v] = the first position with item >= group_begin.
+// counts[v][t] (kGroupMax uint16 per user: two 16-byte halves, tiles 0-7 and 8-15) = the
+// items of user v in tile t of the group ([group_begin + t tile, min(group_begin + (t + 1)
+// tile, stop))), end[v] = the position after the group's last; cur[v] = the first position
+// with item >= group_begin.
 // rec[v] (16 bytes, what k_group_rows gathers per (item, user) pair instead of counts, cur,
 // the class and the items): x = n (the user's items in the group, saturated at 255) |
-// class << 8; for n <= kRecItems the items as 16-bit codes t << 13 | (item - tile t's
-// first item) in y, z, w (low half first); else y = cur[v] (the rows read user_items).
+// class << 8; for n <= kRecItems the items as 16-bit codes t << cs | (item - tile t's first
+// item) in y, z, w (low half first; cs = code_shift(n_tiles): 13 for groups of <= 8 tiles,
+// 12 for more, whose tiles are <= 4096 wide); else y = cur[v] (the rows read user_items).
 constexpr int kRecItems = 6;
+__host__ __device__ constexpr int code_shift(int n_tiles) { return n_tiles <= kGroupWide ? 13 : 12; }
 __global__ __launch_bounds__(256) void k_group_cursor(const int64_t *__restrict__ user_rowptr,
                                                       const int32_t *__restrict__ user_items,
                                                       const uint16_t *__restrict__ user_cls,
@@ -325,80 +329,124 @@ __global__ __launch_bounds__(256) void k_group_cursor(const int64_t *__restrict_
                                                       uint4 *__restrict__ rec) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n_users) return;
+  const int cs = code_shift(n_tiles);
   const int64_t p0 = cur[v];
   int64_t p = p0;
   const int64_t pe = user_rowptr[v + 1];
-  uint32_t c[kGroupMax];
+  // the group's items: [group_begin, glim); an item's tile by one division (a user has few
+  // items in a group: ~1.6 at C5)
+  const int64_t gl = (int64_t)group_begin + (int64_t)n_tiles * tile;
+  const int32_t glim = (int32_t)(gl < stop ? gl : stop);
+  uint32_t c8[kGroupMax / 2];  // per-tile counts, two tiles per word (16-bit fields)
+#pragma unroll
+  for (int h = 0; h < kGroupMax / 2; ++h) c8[h] = 0;
   uint32_t code[kRecItems];
 #pragma unroll
   for (int k = 0; k < kRecItems; ++k) code[k] = 0;
   int n = 0;
+  for (int32_t it = p < pe ? user_items[p] : 0x7fffffff; it < glim;
+       it = p < pe ? user_items[p] : 0x7fffffff) {
+    const uint32_t rel = (uint32_t)(it - group_begin);  // (cur: it >= group_begin)
+    const uint32_t t = rel / (uint32_t)tile;
+    const uint32_t cd = t << cs | (rel - t * (uint32_t)tile);
 #pragma unroll
-  for (int t = 0; t < kGroupMax; ++t) {
-    c[t] = 0;
-    if (t < n_tiles) {
-      const int32_t tb = group_begin + t * tile;
-      const int64_t l = (int64_t)tb + tile;
-      const int32_t lim = (int32_t)(l < stop ? l : stop);
-      const int64_t pt = p;
-      for (; p < pe; ++p) {
-        const int32_t it = user_items[p];
-        if (it >= lim) break;
-        const uint32_t cd = (uint32_t)t << 13 | (uint32_t)(it - tb);
+    for (int k = 0; k < kRecItems; ++k)
+      if (n == k) code[k] = cd;
+    const uint32_t inc = 1u << (16 * (t & 1));
 #pragma unroll
-        for (int k = 0; k < kRecItems; ++k)
-          if (n == k) code[k] = cd;
-        ++n;
-      }
-      c[t] = (uint32_t)(p - pt);  // <= tile <= 8192
-    }
+    for (int h = 0; h < kGroupMax / 2; ++h) c8[h] += t >> 1 == (uint32_t)h ? inc : 0u;
+    ++n;
+    ++p;
   }
-  end[v] = p;
-  counts[v] = uint4{c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16};
+  end[v] = p;  // (the counts of a tile are <= tile <= 8192: no carry between the fields)
+  counts[2 * v] = uint4{c8[0], c8[1], c8[2], c8[3]};
+  counts[2 * v + 1] = uint4{c8[4], c8[5], c8[6], c8[7]};
   const uint32_t hx = (uint32_t)(n < 255 ? n : 255) | (uint32_t)user_cls[v] << 8;
   rec[v] = n <= kRecItems
                ? uint4{hx, code[0] | code[1] << 16, code[2] | code[3] << 16, code[4] | code[5] << 16}
                : uint4{hx, (uint32_t)p0, 0u, 0u};
 }
 
+// tile t's count in a user's 8-tile half c (t < 8)
 __device__ __forceinline__ uint32_t count_of(const uint4 &c, int t) {
   const uint32_t w = t < 2 ? c.x : (t < 4 ? c.y : (t < 6 ? c.z : c.w));
   return (t & 1) ? w >> 16 : w & 0xFFFFu;
 }
+// tile t's count (t < 16) in a user's two halves
+__device__ __forceinline__ uint32_t count_of2(const uint4 &lo, const uint4 &hi, int t) {
+  return t < 8 ? count_of(lo, t) : count_of(hi, t - 8);
+}
 
 // bound[t][i] = sum over the users v of item i of counts[v][t] (the pairs behind row i in
-// tile t). One wave per item row.
+// tile t). 16 lanes per item row, 4 rows per wave (rows of ~100 users fill a 64-lane wave
+// poorly, and a wave's fixed costs -- row pointers, the reduction, the stores -- are then
+// shared by 4 rows). Per round each lane gathers the counts of 8 of its row's users (128 per
+// row; every load is issued, clamped to a valid index, before any is used: one wait for the
+// ids, one for the counts; the second 8-tile half only for groups of more than 8), sums them
+// per tile in 32 bits (<= 8 x 8192), then into 64 bits. The 16 lanes' 16 per-tile sums are
+// reduced by halving exchanges: over xor 8, 4, 2, 1 each lane keeps half of its tiles and
+// adds its partner's sums of those (16 -> 8 -> 4 -> 2 -> 1 tiles): lane t of the row ends
+// with tile t's total (15 shuffles instead of 16 x 4). At C5 the kernel is bound by the
+// random 16-byte count gathers (one per (row, user) pair and group), not by its arithmetic.
+static_assert(kGroupMax == 16, "k_group_bound's halving reduction is written for 16 tiles");
 __global__ __launch_bounds__(256) void k_group_bound(const int64_t *__restrict__ item_rowptr,
                                                      const int32_t *__restrict__ item_users,
                                                      int64_t n_items,
                                                      const uint4 *__restrict__ counts,
                                                      int32_t n_tiles, int64_t *__restrict__ bound) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
-  if (i >= n_items) return;
-  const int lane = lane_id();
-  int64_t s[kGroupMax];
+  constexpr int kU = 8;  // users per lane per round
+  const int lane = lane_id(), sub = lane & 15;
+  const int64_t i = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 4 + (lane >> 4);
+  const bool live = i < n_items;  // (no early exit: the reduction needs every lane)
+  const bool wide = n_tiles > 8;  // (uniform)
+  const int64_t b = live ? item_rowptr[i] : 0, e1 = live ? item_rowptr[i + 1] : 0;
+  uint64_t s[kGroupMax];
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) s[t] = 0;
-  // two 64-user chunks per iteration: both gathers in flight together
-  const int64_t e1 = item_rowptr[i + 1];
-  for (int64_t b = item_rowptr[i]; b < e1; b += 128) {
-    const int64_t e = b + lane;
-    const bool in0 = e < e1, in1 = e + 64 < e1;
-    const int32_t v0 = in0 ? item_users[e] : 0, v1 = in1 ? item_users[e + 64] : 0;
-    uint4 c0{0u, 0u, 0u, 0u}, c1{0u, 0u, 0u, 0u};
-    if (in0) c0 = counts[v0];
-    if (in1) c1 = counts[v1];
+  // (a round runs only while some row of the wave has users left: there are interactions,
+  // so index 0 of item_users and of counts is valid for the clamped lanes)
+  for (int64_t r0 = b; __ballot(r0 < e1) != 0; r0 += 16 * kU) {
+    int32_t v[kU];
 #pragma unroll
-    for (int t = 0; t < kGroupMax; ++t) s[t] += count_of(c0, t) + count_of(c1, t);
-  }
-#pragma unroll
-  for (int t = 0; t < kGroupMax; ++t) {
-    if (t < n_tiles) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s[t] += __shfl_xor(s[t], o);
-      if (lane == 0) bound[(int64_t)t * n_items + i] = s[t];
+    for (int u = 0; u < kU; ++u) {
+      const int64_t e = r0 + sub + 16 * u;
+      v[u] = item_users[e < e1 ? e : 0];
     }
+    uint4 cl[kU], ch[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      cl[u] = counts[2 * (int64_t)v[u]];
+      ch[u] = wide ? counts[2 * (int64_t)v[u] + 1] : uint4{0u, 0u, 0u, 0u};
+    }
+    uint32_t rs[kGroupMax];
+#pragma unroll
+    for (int t = 0; t < kGroupMax; ++t) rs[t] = 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const bool in = r0 + sub + 16 * u < e1;
+      const uint4 zl = in ? cl[u] : uint4{0u, 0u, 0u, 0u};
+      const uint4 zh = in ? ch[u] : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int t = 0; t < kGroupMax; ++t) rs[t] += count_of2(zl, zh, t);
+    }
+#pragma unroll
+    for (int t = 0; t < kGroupMax; ++t) s[t] += rs[t];
   }
+  // halving exchanges within the row's 16 lanes: after the step over xor m the lane keeps
+  // the tiles whose bit (m) equals its own
+  uint64_t r8[8], r4[4], r2[2];
+  const bool h3 = sub & 8, h2 = sub & 4, h1 = sub & 2, h0 = sub & 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    r8[j] = (h3 ? s[j + 8] : s[j]) + __shfl_xor(h3 ? s[j] : s[j + 8], 8);  // tiles 8 h3 + j
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    r4[j] = (h2 ? r8[j + 4] : r8[j]) + __shfl_xor(h2 ? r8[j] : r8[j + 4], 4);  // + 4 h2 + j
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    r2[j] = (h1 ? r4[j + 2] : r4[j]) + __shfl_xor(h1 ? r4[j] : r4[j + 2], 2);  // + 2 h1 + j
+  const uint64_t r1 = (h0 ? r2[1] : r2[0]) + __shfl_xor(h0 ? r2[0] : r2[1], 1);  // + h0
+  if (live && sub < n_tiles) bound[(int64_t)sub * n_items + i] = (int64_t)r1;
 }
 
 // Overflow units (run header + data) of a row with nb pairs in a tile of width w: P rows
@@ -431,10 +479,39 @@ __global__ __launch_bounds__(256) void k_group_units(const int64_t *__restrict__
   units[x] = run_units(bound[x], vthr, tile_width(group_begin, tile, t, stop));
 }
 
+// Inclusive prefix sum over the wave's 64 lanes by DPP (no LDS round trips): row_shr 1, 2,
+// 4, 8 inside each 16-lane row, then row_bcast 15 / 31 add the earlier rows' totals.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+// lane t's 64-bit value as a wave-uniform scalar
+__device__ __forceinline__ int64_t readlane64(int64_t x, int t) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, t);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), t);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // P rows of every tile of the group: one wave per item row (tiles whose row is a hub row,
-// bound > vthr, are left to k_group_rows_hub). The lanes' counts of two tiles are scanned
-// together as 16-bit fields of one word: a P row's prefix never exceeds its bound <= vthr <
-// 2^16, and hub tiles' counts are masked to 0 before the scan.
+// bound > vthr, are left to k_group_rows_hub). The row's lines (kGroupMax x 128 bytes) are
+// assembled in the wave's LDS and written with two coalesced 16-byte-per-lane stores at the
+// end (the slots of a line come from ~20 lanes over several chunks: written straight to
+// global memory they took ~5 sparse store instructions per (row, tile)); slots past a line's
+// 31 go to the overflow run directly. Per chunk of 64 users (lane = user, ascending): the
+// user's per-tile item counts (from its record's item codes, or its counts for users with
+// more than kRecItems items in the group), two tiles per word as 16-bit fields (a P row's
+// prefix never exceeds its bound <= vthr < 2^16; hub tiles' counts are masked to 0), one
+// DPP prefix sum per word; then per tile t the lane's first slot position minus its item
+// index in the group, D_t (an LDS table, [t][lane]), so each of the lane's items k lands
+// at slot D_t + k with one table read -- one pass over the user's items instead of one per
+// tile. A chunk's user records are gathered one chunk ahead and its users two ahead
+// (unconditional loads, clamped into the row).
 __global__ __launch_bounds__(256) void k_group_rows(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int32_t *__restrict__ user_items, int64_t n_items, const uint4 *__restrict__ counts,
@@ -442,8 +519,12 @@ __global__ __launch_bounds__(256) void k_group_rows(
     int32_t stop, const int64_t *__restrict__ bound, int64_t vthr,
     const int64_t *__restrict__ units_incl,
     uint32_t *__restrict__ lines, uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
-  if (i >= n_items) return;
+  __shared__ __attribute__((aligned(16))) uint32_t s_line[4][kGroupMax * 32];
+  __shared__ uint32_t s_pos[4][kGroupMax][64];
+  __shared__ uint32_t s_ovw[4][kGroupMax];  // tile t's run: its first data word in ovf
+  const int wv = threadIdx.x / 64;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wv;
+  if (i >= n_items) return;  // (whole waves: the LDS is per wave, no block barrier)
   const int lane = lane_id();
   // lane t < n_tiles: row i's pairs, run offset (relative to the tile's runs) and the
   // tile's first unit in ovf
@@ -454,134 +535,158 @@ __global__ __launch_bounds__(256) void k_group_rows(
     obl = lane ? units_incl[(int64_t)lane * n_items - 1] : 0;
     oul = units_incl[x] - run_units(nbl, vthr, tile_width(group_begin, tile, lane, stop)) - obl;
   }
-  const int64_t tstride = (n_items + 1) * 32;  // words per tile of lines
-  // P tiles of this row (wave-uniform)
-  const uint32_t pmask = (uint32_t)__ballot(lane < n_tiles && nbl <= vthr);
-  for (int t = 0; t < n_tiles; ++t) {
-    if (!((pmask >> t) & 1)) continue;
-    const int64_t nb = __shfl(nbl, t);
-    const bool has_ovf = nb > kLineSlots;
-    const int64_t ou = has_ovf ? __shfl(oul, t) : 0;
-    uint32_t *line = lines + (int64_t)t * tstride + i * 32;
-    uint32_t *ov = ovf + __shfl(obl, t) * 4;
-    const int64_t n_units = has_ovf ? (nb - kLineSlots + 3) / 4 : 0;
-    const int64_t cap = kLineSlots + 4 * n_units;
-    if (has_ovf && lane < 4) ov[ou * 4 + lane] = lane == 0 ? (uint32_t)n_units : 0u;
-    for (int64_t p = nb + lane; p < cap; p += 64) put_slot(line, ov, ou, p, 0u);
+  const int64_t eb = item_rowptr[i], e1 = item_rowptr[i + 1];
+  const int cs = code_shift(n_tiles);
+  const uint32_t cmask = (1u << cs) - 1u;
+  const bool wide = n_tiles > 8;  // (uniform)
+  uint32_t *line_s = s_line[wv];
+  {  // the lines start all zero (padding); 2 x 16 bytes per lane
+    uint4 *l4 = reinterpret_cast<uint4 *>(line_s);
+    l4[lane] = uint4{0u, 0u, 0u, 0u};
+    l4[64 + lane] = uint4{0u, 0u, 0u, 0u};
   }
-  uint32_t n[kGroupMax];  // pairs written so far per tile (P rows: <= vthr < 2^16)
+  wave_sync();
+  const bool has_run_l = lane < n_tiles && nbl <= vthr && nbl > kLineSlots;
+  if (lane < n_tiles) s_ovw[wv][lane] = (uint32_t)((obl + oul + 1) * 4);
+  uint32_t pmask = 0;  // P tiles of this row (uniform)
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t)
+    if (t < n_tiles && readlane64(nbl, t) <= vthr) pmask |= 1u << t;
+  // overflow runs of the P tiles: header unit and the padding past the row's pairs
+  uint32_t runs = (uint32_t)__ballot(has_run_l);
+  while (runs) {
+    const int t = __builtin_ctz(runs);
+    runs &= runs - 1;
+    const int64_t nb = readlane64(nbl, t);
+    const int64_t ob = readlane64(obl, t) + readlane64(oul, t);  // the run's header unit
+    const int64_t n_units = (nb - kLineSlots + 3) / 4;
+    if (lane < 4) ovf[ob * 4 + lane] = lane == 0 ? (uint32_t)n_units : 0u;
+    for (int64_t p = nb + lane; p < kLineSlots + 4 * n_units; p += 64)
+      ovf[(ob + 1) * 4 + (p - kLineSlots)] = 0u;
+  }
+  uint32_t m8[kGroupMax / 2];
+#pragma unroll
+  for (int h = 0; h < kGroupMax / 2; ++h) {
+    const uint32_t lo = ((pmask >> (2 * h)) & 1) ? 0xFFFFu : 0u;
+    const uint32_t hi = ((pmask >> (2 * h + 1)) & 1) ? 0xFFFF0000u : 0u;
+    m8[h] = lo | hi;
+  }
+  uint32_t n[kGroupMax];  // pairs written so far per tile (uniform)
 #pragma unroll
   for (int t = 0; t < kGroupMax; ++t) n[t] = 0;
   uint32_t farbits = 0;
-  const int64_t e1 = item_rowptr[i + 1];
-  // the next chunk's users and records are gathered while this chunk is written
-  uint4 rcn{0u, 0u, 0u, 0u};
-  int32_t vn = 0;
-  {
-    const int64_t e = item_rowptr[i] + lane;
-    if (e < e1) {
-      vn = item_users[e];
-      rcn = rec[vn];
-    }
+  auto user_at = [&](int64_t e0) __attribute__((always_inline)) {
+    const int64_t e = e0 + lane;
+    return item_users[e < e1 ? e : e1 - 1];
+  };
+  int32_t v_c = 0, v_n = 0;
+  uint4 r_c{0u, 0u, 0u, 0u};
+  if (eb < e1) {
+    v_c = user_at(eb);
+    v_n = user_at(eb + 64);
+    r_c = rec[v_c];
   }
-  for (int64_t e0 = item_rowptr[i]; e0 < e1; e0 += 64) {
-    const uint4 rc = rcn;
-    const int32_t v = vn;
-    if (e0 + 64 < e1) {
-      const int64_t e = e0 + 64 + lane;
-      rcn = uint4{0u, 0u, 0u, 0u};
-      vn = 0;
-      if (e < e1) {
-        vn = item_users[e];
-        rcn = rec[vn];
-      }
-    }
-    const uint32_t nu = rc.x & 0xFFu;  // the user's items in the group
+  for (int64_t e0 = eb; e0 < e1; e0 += 64) {
+    const int32_t v = v_c;
+    const uint4 rc = e0 + lane < e1 ? r_c : uint4{0u, 0u, 0u, 0u};
+    const uint32_t nu = rc.x & 0xFFu;  // the user's items in the group (saturated)
     const bool longu = nu > (uint32_t)kRecItems;
-    uint4 c4{0u, 0u, 0u, 0u};
+    uint32_t c8[kGroupMax / 2];  // the user's per-tile counts, two tiles per word
+#pragma unroll
+    for (int h = 0; h < kGroupMax / 2; ++h) c8[h] = 0;
+    // (the rare users with more items than the record holds load their counts before the
+    // prefetch below is issued: waiting for these loads then drains nothing younger)
     if (longu) {
-      c4 = counts[v];
-    } else {  // per-tile counts from the item codes (ascending: tiles in order)
+      const uint4 lo = counts[2 * (int64_t)v];
+      const uint4 hi = wide ? counts[2 * (int64_t)v + 1] : uint4{0u, 0u, 0u, 0u};
+      c8[0] = lo.x, c8[1] = lo.y, c8[2] = lo.z, c8[3] = lo.w;
+      c8[4] = hi.x, c8[5] = hi.y, c8[6] = hi.z, c8[7] = hi.w;
+    }
+    v_c = v_n;
+    r_c = rec[v_n];           // the next chunk's records
+    v_n = user_at(e0 + 128);  // the users of the one after
+    if (!longu) {  // per-tile counts from the item codes
 #pragma unroll
       for (int k = 0; k < kRecItems; ++k) {
         const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
         const uint32_t cd = (k & 1) ? wd >> 16 : wd & 0xFFFFu;
         if ((uint32_t)k < nu) {
-          const uint32_t t = cd >> 13;
+          const uint32_t t = cd >> cs;
           const uint32_t inc = 1u << (16 * (t & 1));
-          c4.x += t >> 1 == 0 ? inc : 0u;
-          c4.y += t >> 1 == 1 ? inc : 0u;
-          c4.z += t >> 1 == 2 ? inc : 0u;
-          c4.w += t >> 1 == 3 ? inc : 0u;
+#pragma unroll
+          for (int h = 0; h < kGroupMax / 2; ++h) c8[h] += t >> 1 == (uint32_t)h ? inc : 0u;
         }
       }
     }
-    // hub tiles' counts masked out (their items still advance the lane's offset)
-    uint32_t m4[4];
+    uint32_t any = 0;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const uint32_t lo = ((pmask >> (2 * h)) & 1) ? 0xFFFFu : 0u;
-      const uint32_t hi = ((pmask >> (2 * h + 1)) & 1) ? 0xFFFF0000u : 0u;
-      m4[h] = lo | hi;
-    }
-    const uint32_t w[4] = {c4.x & m4[0], c4.y & m4[1], c4.z & m4[2], c4.w & m4[3]};
-    if (__ballot((w[0] | w[1] | w[2] | w[3]) != 0) == 0) continue;  // no pair in any P tile
-    const int64_t s0 = longu ? (int64_t)rc.y : 0;
-    const uint32_t cl = rc.x >> 8;
-    uint32_t off = 0;
+    for (int h = 0; h < kGroupMax / 2; ++h) any |= c8[h] & m8[h];
+    if (__ballot(any != 0) == 0) continue;  // no pair in any P tile
+    // D_t per tile: (pairs before this chunk) + (this chunk's lanes before this one) - (the
+    // user's items in tiles < t)
+    uint32_t off = 0, ntot = 0;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
+    for (int h = 0; h < kGroupMax / 2; ++h) {
       if (2 * h >= n_tiles) break;
-      uint32_t pre = w[h];
-      if (__ballot(pre != 0) != 0) {
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(pre, o);
-          if (lane >= o) pre += y;
-        }
-      }
-      const uint32_t total = __shfl(pre, 63);
-      pre -= w[h];
+      const uint32_t wm = c8[h] & m8[h];
+      uint32_t pre = wm;
+      if (__ballot(pre != 0) != 0) pre = wave_incl_sum(pre);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)pre, 63);
+      pre -= wm;
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int t = 2 * h + b;
-        const uint32_t ct = (w[h] >> (16 * b)) & 0xFFFFu;
-        const uint32_t tot = (total >> (16 * b)) & 0xFFFFu;
-        if (tot) {
-          const uint32_t pb = (pre >> (16 * b)) & 0xFFFFu;
-          uint32_t *line = lines + (int64_t)t * tstride + i * 32;
-          uint32_t *ov = ovf + __shfl(obl, t) * 4;
-          const int64_t ou = __shfl(oul, t);
-          const int32_t ib = group_begin + t * tile;
-          for (uint32_t q = 0; q < ct; ++q) {
-            uint32_t jr;
-            if (longu) {
-              jr = (uint32_t)(user_items[s0 + off + q] - ib);
-            } else {
-              const uint32_t k = off + q;
-              const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
-              jr = ((k & 1) ? wd >> 16 : wd) & 0x1FFFu;
-            }
-            put_slot(line, ov, ou, (int64_t)(n[t] + pb + q), (cl << 16) | jr);
-          }
-          if (ct && cl >= (uint32_t)kInvTab) farbits |= 1u << t;
-          n[t] += tot;
-        }
-        off += count_of(c4, t);
+        const uint32_t pb = (pre >> (16 * b)) & 0xFFFFu;
+        s_pos[wv][t][lane] = n[t] + pb - off;
+        n[t] += (total >> (16 * b)) & 0xFFFFu;
+        off += (c8[h] >> (16 * b)) & 0xFFFFu;
+      }
+    }
+    ntot = off;  // the user's items in the group's tiles (all of them, n_tiles <= 16)
+    wave_sync();
+    const int64_t s0 = longu ? (int64_t)rc.y : 0;
+    const uint32_t cl = rc.x >> 8;
+    uint32_t tl = 0;  // (long users: the tile of the current item, items ascending)
+    for (uint32_t k = 0; k < ntot; ++k) {
+      uint32_t t, col;
+      if (!longu) {
+        const uint32_t wd = k < 2 ? rc.y : (k < 4 ? rc.z : rc.w);
+        const uint32_t cd = (k & 1) ? wd >> 16 : wd & 0xFFFFu;
+        t = cd >> cs;
+        col = cd & cmask;
+      } else {
+        const uint32_t rel = (uint32_t)(user_items[s0 + k] - group_begin);
+        while (rel >= (tl + 1) * (uint32_t)tile) ++tl;
+        t = tl;
+        col = rel - tl * (uint32_t)tile;
+      }
+      if ((pmask >> t) & 1u) {
+        const uint32_t pos = s_pos[wv][t][lane] + k;
+        const uint32_t word = (cl << 16) | col;
+        if (pos < (uint32_t)kLineSlots) line_s[t * 32 + 1 + pos] = word;
+        else ovf[(int64_t)s_ovw[wv][t] + (pos - kLineSlots)] = word;
+        if (cl >= (uint32_t)kInvTab) farbits |= 1u << t;
       }
     }
   }
-  for (int t = 0; t < n_tiles; ++t) {
-    if (!((pmask >> t) & 1)) continue;
-    const bool slow = __ballot((farbits >> t) & 1) != 0;
-    const int64_t nb = __shfl(nbl, t);
-    const bool has_ovf = nb > kLineSlots;
-    const int64_t ou = __shfl(oul, t);
-    if (lane == 0) {
-      lines[(int64_t)t * tstride + i * 32] =
-          (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u) | (slow ? kHdrSlow : 0u);
-      if (row_len) row_len[(int64_t)t * n_items + i] = (int32_t)nb;
-    }
+  // headers (lane t: tile t) and row lengths, then the lines
+  uint32_t slowm = 0;
+#pragma unroll
+  for (int t = 0; t < kGroupMax; ++t)
+    if ((pmask >> t) & 1u) slowm |= __ballot((farbits >> t) & 1u) != 0 ? 1u << t : 0u;
+  if (lane < kGroupMax && ((pmask >> lane) & 1u)) {
+    line_s[lane * 32] = (nbl > kLineSlots ? (kHdrOvf | (uint32_t)oul) : 0u) |
+                        (((slowm >> lane) & 1u) ? kHdrSlow : 0u);
+    if (row_len) row_len[(int64_t)lane * n_items + i] = (int32_t)nbl;
+  }
+  wave_sync();
+  const int64_t tstride = (n_items + 1) * 32;  // words per tile of lines
+#pragma unroll
+  for (int r = 0; r < kGroupMax / 8; ++r) {
+    const int t = 8 * r + (lane >> 3), u = lane & 7;
+    if ((pmask >> t) & 1u)
+      *reinterpret_cast<uint4 *>(lines + (int64_t)t * tstride + i * 32 + 4 * u) =
+          reinterpret_cast<const uint4 *>(line_s)[t * 8 + u];
   }
 }
 
@@ -608,11 +713,11 @@ __global__ __launch_bounds__(256) void k_group_rows_hub(
     __syncthreads();
     for (int64_t e = item_rowptr[i]; e < item_rowptr[i + 1]; ++e) {
       const int32_t v = item_users[e];
-      const uint4 c4 = counts[v];
-      const int c = (int)count_of(c4, t);
+      const uint4 lo = counts[2 * (int64_t)v], hi = counts[2 * (int64_t)v + 1];
+      const int c = (int)count_of2(lo, hi, t);
       if (c == 0) continue;  // uniform across the block: no barrier skipped unevenly
       int64_t s0 = cur[v];
-      for (int q = 0; q < t; ++q) s0 += count_of(c4, q);
+      for (int q = 0; q < t; ++q) s0 += count_of2(lo, hi, q);
       const double wv = inv_deg[v];
       for (int q = threadIdx.x; q < c; q += blockDim.x) acc[user_items[s0 + q] - item_begin] += wv;
       __syncthreads();  // the next user may hit the same columns from other threads
@@ -1967,8 +2072,10 @@ extern "C" int lg_spread_group_cursor(const int64_t *user_rowptr, const int32_t 
                  cur != end && group_begin >= 0 && stop > group_begin,
              "lg_spread_group_cursor: bad arguments");
   LG_REQUIRE(((uintptr_t)rec & 15) == 0, "lg_spread_group_cursor: rec not 16-byte aligned");
-  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
-             "lg_spread_group_cursor: tile %d / n_tiles %d", tile, n_tiles);
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax &&
+                 (n_tiles <= kGroupWide || tile <= 4096),
+             "lg_spread_group_cursor: tile %d / n_tiles %d (groups of more than %d tiles need tile <= 4096)",
+             tile, n_tiles, kGroupWide);
   LG_REQUIRE(((uintptr_t)counts & 15) == 0, "lg_spread_group_cursor: counts not 16-byte aligned");
   if (n_users == 0) return LG_OK;
   k_group_cursor<<<dim3((unsigned)((n_users + 255) / 256)), dim3(256), 0,
@@ -1985,7 +2092,7 @@ extern "C" int lg_spread_group_bound(const int64_t *item_rowptr, const int32_t *
                  n_tiles <= kGroupMax && ((uintptr_t)counts & 15) == 0,
              "lg_spread_group_bound: bad arguments");
   if (n_items == 0) return LG_OK;
-  k_group_bound<<<dim3((unsigned)((n_items + 3) / 4)), dim3(256), 0, (hipStream_t)stream>>>(
+  k_group_bound<<<dim3((unsigned)((n_items + 15) / 16)), dim3(256), 0, (hipStream_t)stream>>>(
       item_rowptr, item_users, n_items, (const uint4 *)counts, n_tiles, bound);
   return launch_status("lg_spread_group_bound");
 }
@@ -1996,8 +2103,10 @@ extern "C" int lg_spread_group_units(const int64_t *bound, int64_t n_items, int3
   LG_REQUIRE(bound && units && n_items >= 0 && group_begin >= 0 && stop > group_begin &&
                  vthr >= kLineSlots,
              "lg_spread_group_units: bad arguments");
-  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
-             "lg_spread_group_units: tile %d / n_tiles %d", tile, n_tiles);
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax &&
+                 (n_tiles <= kGroupWide || tile <= 4096),
+             "lg_spread_group_units: tile %d / n_tiles %d (groups of more than %d tiles need tile <= 4096)",
+             tile, n_tiles, kGroupWide);
   const int64_t n = n_items * n_tiles;
   if (n == 0) return LG_OK;
   k_group_units<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream>>>(
@@ -2020,8 +2129,10 @@ extern "C" int lg_spread_group_rows_f64(
              "lg_spread_group_rows_f64: bad arguments");
   LG_REQUIRE(vthr >= kLineSlots && vthr < 65536,
              "lg_spread_group_rows_f64: vthr %lld not in [31, 65535]", (long long)vthr);
-  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax,
-             "lg_spread_group_rows_f64: tile %d / n_tiles %d", tile, n_tiles);
+  LG_REQUIRE(tile >= 1 && tile <= 8192 && n_tiles >= 1 && n_tiles <= kGroupMax &&
+                 (n_tiles <= kGroupWide || tile <= 4096),
+             "lg_spread_group_rows_f64: tile %d / n_tiles %d (groups of more than %d tiles need tile <= 4096)",
+             tile, n_tiles, kGroupWide);
   LG_REQUIRE(((uintptr_t)counts & 15) == 0, "lg_spread_group_rows_f64: counts not 16-byte aligned");
   if (n_items == 0) return LG_OK;
   const size_t need = lg_spread_group_rows_ws_bytes(n_items, n_tiles);

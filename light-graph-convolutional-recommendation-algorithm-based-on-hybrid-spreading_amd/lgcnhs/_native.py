@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("LGCNHS_LIB_PATH") or LIB_PATH
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64

@@ -399,6 +399,7 @@ def spread_topk(A: Interactions, W: torch.Tensor, k: int, excl: RowSets | None,
 INV_TAB = 512      # degree classes cached in LDS by the walk (csrc/spread_tiled.hip)
 MAX_CLASSES = 0x7FFF   # P slot words keep bit 31 clear (it marks V entries)
 LINE_SLOTS, LINE_ENTS = 31, 7   # P slots / V entries in a row's 128-byte line
+GROUP_MAX, GROUP_WIDE = 16, 8   # tiles per group build (tiles wider than 4096: 8)
 
 
 def hybrid_recip(k_item: torch.Tensor, lam: float):
@@ -467,9 +468,9 @@ class TileWeights:
     reused and grown on demand. ``vthr``: rows with more pairs are V rows (default: the tile
     width).
 
-    Tiles are built ``group`` at a time (1..8, default 8): lg_spread_group_cursor / _bound /
-    _units / _rows_f64 visit each (item row, user) pair once per group instead of once per
-    tile and write the group's tiles side by side; build(j0) of a tile inside the built
+    Tiles are built ``group`` at a time (1..16, default 16; at most 8 for tiles wider than
+    4096): lg_spread_group_cursor / _bound / _units / _rows_f64 visit each (item row, user)
+    pair once per group instead of once per tile and write the group's tiles side by side; build(j0) of a tile inside the built
     group only selects it. Every tile's words are those of the per-tile reference build
     (include/lgcnhs_ref.h) bit for bit (tests/test_gpu_spread_tiled.py)."""
 
@@ -483,10 +484,11 @@ class TileWeights:
         if vthr is None:
             vthr = self.tile
         self.vthr = max(LINE_SLOTS, int(vthr))
+        gmax = GROUP_MAX if self.tile <= 4096 else GROUP_WIDE
         if group is None:
-            group = 8
-        if not 1 <= group <= 8:
-            raise ValueError(f"group {group} not in [1, 8]")
+            group = gmax
+        if not 1 <= group <= gmax:
+            raise ValueError(f"group {group} not in [1, {gmax}] (tile {self.tile})")
         if self.vthr > 65535:
             raise ValueError(f"vthr {self.vthr} > 65535 (the group build counts 16-bit)")
         I = A.n_items
@@ -494,11 +496,12 @@ class TileWeights:
         S = self.group
         self.cur = A.by_user.rowptr[:-1].contiguous().clone()
         self.end = torch.empty_like(self.cur)
-        # 8 uint16 per user (one 16-byte load) + the rows pass's 16-byte records
+        # 16 uint16 per user (two 16-byte halves: tiles 0-7, 8-15) + the rows pass's 16-byte
+        # records
         if int(A.by_user.rowptr[-1]) >= 1 << 32:
             raise ValueError("more than 2^32 interactions: the group build's positions are "
                              "32-bit")
-        self.counts = torch.empty((A.n_users, 8), dtype=torch.uint16, device=dev)
+        self.counts = torch.empty((A.n_users, GROUP_MAX), dtype=torch.uint16, device=dev)
         self.rec = torch.empty((A.n_users, 4), dtype=torch.int32, device=dev)
         self.inv_deg = torch.empty(A.n_users, dtype=torch.float64, device=dev)
         N.check(N.lib().lg_inv_degree_f64(N.ptr(A.by_user.rowptr), A.n_users,

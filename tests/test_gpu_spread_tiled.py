@@ -74,7 +74,8 @@ def test_tile_weights_and_resource(zipf, lam):
 
 @pytest.mark.parametrize("zipf,tile,group,vthr", [(False, 64, 8, None), (True, 100, 3, None),
                                                   (True, 256, 8, None), (True, 128, 5, 40),
-                                                  (False, 1000, 8, None)])
+                                                  (False, 1000, 8, None), (False, 40, 16, None),
+                                                  (True, 50, 11, None), (True, 33, 16, 35)])
 def test_group_build_equals_per_tile(zipf, tile, group, vthr):
     """The group build (lg_spread_group_*: each (item, user) pair visited once per group of
     tiles) writes every tile's lines, overflow runs, bounds and row lengths bit for bit as the
@@ -170,6 +171,10 @@ def test_tile_api_errors():
     A = _inter(50, 60, 500, seed=1)
     with pytest.raises(ValueError):
         ops.TileWeights(A, 0.5, 0)
+    with pytest.raises(ValueError):  # groups of more than 8 tiles: tiles <= 4096 wide
+        ops.TileWeights(A, 0.5, 5000, group=16)
+    with pytest.raises(ValueError):
+        ops.TileWeights(A, 0.5, 16, group=17)
     tw = ops.TileWeights(A, 0.5, 16)
     tw.build(0)
     with pytest.raises(ValueError):
