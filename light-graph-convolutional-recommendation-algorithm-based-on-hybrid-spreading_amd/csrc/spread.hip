@@ -116,41 +116,49 @@ __device__ __forceinline__ float chain_score(const float *__restrict__ us,
   return acc;
 }
 
-// One wave per row. D == 0: no G factor.
-template <int M, int D>
-__global__ __launch_bounds__(256) void k_rows_topk(
+// NW waves per row (one row per block), D == 0: no G factor. Wave w scans the row's w-th
+// column range (whole 64-column steps) in ascending order into its own candidate list --
+// at the C3 Douban shape (600 rows x 20,000 columns) one wave per row left the chip mostly
+// idle behind each step's load -> 64-FMA chain latency -- then the waves' top-k lists merge
+// pairwise in log2(NW) rounds (each merge: the partner's <= k entries appended, the list
+// compacted; the (value desc, column asc) order is total, so the result is the single
+// scan's). Columns arrive in ascending order within a wave, so a tie with tau loses.
+template <int M, int D, int NW>
+__global__ __launch_bounds__(64 * NW) void k_rows_topk(
     const double *__restrict__ F, int64_t ldf, int64_t n_rows, int64_t n_cols,
     const float *__restrict__ eu, const float *__restrict__ ei,
     const int64_t *__restrict__ ex_rowptr, const int32_t *__restrict__ ex_col, int excl_mode,
     int k, double *__restrict__ out_val, int64_t *__restrict__ out_idx) {
   constexpr int CAP = 64 * M;
   constexpr int DU = D > 0 ? D : 1;
-  __shared__ double cs[4][CAP];
-  __shared__ int ci[4][CAP];
-  __shared__ float us[4][DU];
+  static_assert(CAP >= 128 && (NW & (NW - 1)) == 0, "a merge holds two lists of k <= CAP / 2");
+  __shared__ double cs[NW][CAP];
+  __shared__ int ci[NW][CAP];
+  __shared__ float us[DU];
+  __shared__ int s_n[NW];
   const int wave = threadIdx.x / 64;
   const int lane = lane_id();
-  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
-  if (r >= n_rows) return;
+  const int64_t r = blockIdx.x;  // (< n_rows: one block per row)
   if (D > 0) {
-    for (int t = lane; t < D; t += 64) us[wave][t] = eu[r * D + t];
-    wave_sync();
+    for (int t = threadIdx.x; t < D; t += 64 * NW) us[t] = eu[r * D + t];
+    __syncthreads();
   }
   int64_t lo = 0, hi = 0;
   if (ex_rowptr && excl_mode == LG_EXCL_DROP) {
     lo = ex_rowptr[r];
     hi = ex_rowptr[r + 1];
   }
+  const int64_t span = ((n_cols + NW - 1) / NW + 63) / 64 * 64;
+  const int64_t c0 = wave * span, c1 = c0 + span < n_cols ? c0 + span : n_cols;
   int cnt = 0;
   double tau = neg_inf<double>();
   int tau_id = kPadId;
   const double *row = F + r * ldf;
-  for (int64_t j0 = 0; j0 < n_cols; j0 += 64) {
+  for (int64_t j0 = c0; j0 < c1; j0 += 64) {
     const int64_t j = j0 + lane;
-    const bool valid = j < n_cols;
+    const bool valid = j < c1;
     double v = valid ? row[j] : neg_inf<double>();
-    if (D > 0 && valid) v = (double)chain_score<DU>(us[wave], ei + j * D) * v;
-    // columns arrive in ascending order, so a tie with tau loses: plain '>' is exact
+    if (D > 0 && valid) v = (double)chain_score<DU>(us, ei + j * D) * v;
     bool cand = valid && v > tau;
     if (__ballot(cand)) {
       if (cand && lo < hi) {
@@ -172,10 +180,44 @@ __global__ __launch_bounds__(256) void k_rows_topk(
     }
   }
   wave_sync();
-  const int nc = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
-  for (int e = lane; e < k; e += 64) {
-    out_val[r * k + e] = e < nc ? cs[wave][e] : neg_inf<double>();
-    out_idx[r * k + e] = e < nc ? ci[wave][e] : -1;
+  int nc = wave_compact<double, M>(cs[wave], ci[wave], cnt, k, tau, tau_id);
+  if (lane == 0) s_n[wave] = nc;
+#pragma unroll
+  for (int st = 1; st < NW; st <<= 1) {
+    __syncthreads();
+    if (wave % (2 * st) == 0) {  // (wave + st < NW: NW is a power of two)
+      const int n1 = s_n[wave + st];
+      for (int e = lane; e < n1; e += 64) {
+        cs[wave][nc + e] = cs[wave + st][e];
+        ci[wave][nc + e] = ci[wave + st][e];
+      }
+      wave_sync();
+      nc = wave_compact<double, M>(cs[wave], ci[wave], nc + n1, k, tau, tau_id);
+      if (lane == 0) s_n[wave] = nc;
+    }
+  }
+  if (wave == 0) {
+    for (int e = lane; e < k; e += 64) {
+      out_val[r * k + e] = e < nc ? cs[0][e] : neg_inf<double>();
+      out_idx[r * k + e] = e < nc ? ci[0][e] : -1;
+    }
+  }
+}
+
+// rows of at least this many columns get 8 waves each, shorter ones one
+constexpr int64_t kRowsSplitCols = 4096;
+
+template <int M, int NW>
+static void launch_rows_topk_nw(int dim, const double *F, int64_t ldf, int64_t n_rows,
+                                int64_t n_cols, const float *eu, const float *ei,
+                                const int64_t *ex_rowptr, const int32_t *ex_col, int excl_mode,
+                                int k, double *out_val, int64_t *out_idx, hipStream_t s) {
+  dim3 grid((unsigned)n_rows), block(64 * NW);
+  switch (eu ? dim : 0) {
+    case 0: k_rows_topk<M, 0, NW><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    case 32: k_rows_topk<M, 32, NW><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    case 64: k_rows_topk<M, 64, NW><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
+    default: k_rows_topk<M, 128, NW><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
   }
 }
 
@@ -184,13 +226,12 @@ static void launch_rows_topk(int dim, const double *F, int64_t ldf, int64_t n_ro
                              int64_t n_cols, const float *eu, const float *ei,
                              const int64_t *ex_rowptr, const int32_t *ex_col, int excl_mode,
                              int k, double *out_val, int64_t *out_idx, hipStream_t s) {
-  dim3 grid((unsigned)((n_rows + 3) / 4)), block(256);
-  switch (eu ? dim : 0) {
-    case 0: k_rows_topk<M, 0><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
-    case 32: k_rows_topk<M, 32><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
-    case 64: k_rows_topk<M, 64><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
-    default: k_rows_topk<M, 128><<<grid, block, 0, s>>>(F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode, k, out_val, out_idx); break;
-  }
+  if (n_cols >= kRowsSplitCols)
+    launch_rows_topk_nw<M, 8>(dim, F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode,
+                              k, out_val, out_idx, s);
+  else
+    launch_rows_topk_nw<M, 1>(dim, F, ldf, n_rows, n_cols, eu, ei, ex_rowptr, ex_col, excl_mode,
+                              k, out_val, out_idx, s);
 }
 
 }  // namespace lg
