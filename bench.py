@@ -636,10 +636,10 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, e
 
 def bench_dense_spread(dev, k, lam):
     """configs[2] stand-in: Douban-like (U=600, I=20000, 60000 Zipf(1.1) interactions), the
-    dense spreading path (general_W and W as fp64 I x I matrices, fused G * F top-k), end to
-    end and per kernel with HIP events, each against its roofline (algorithmic bytes / HBM
-    peak; general_W: the I x I write, hybrid: read + write, resource: the W rows gathered per
-    (user, item) + the F write, rows top-k: the F read)."""
+    dense spreading path of spread_recommend (W as an fp64 I x I matrix built with general_W
+    in one pass, fused G * F top-k), end to end and per kernel with HIP events, each against
+    its roofline (algorithmic bytes / HBM peak; general_W + HybridS: the I x I write,
+    resource: the W rows gathered per (user, item) + the F write, rows top-k: the F read)."""
     from lgcnhs import ops
     from lgcnhs.synth import synth_interactions
     du, di, de = 600, 20_000, 60_000
@@ -654,37 +654,32 @@ def bench_dense_spread(dev, k, lam):
         Ad = ops.Interactions.from_pairs(torch.as_tensor(users), torch.as_tensor(items), du,
                                          di, dev)
         mark(1)
-        gW = ops.spread_general(Ad)
+        W = ops.spread_hybrid(Ad, lam)  # general_W + HybridS, one pass (spread_recommend's)
         mark(2)
-        W = ops.hybrid_weight(gW, Ad.k_item, lam)
-        del gW
-        mark(3)
         F = ops.spread_resource(Ad, W)
-        mark(4)
+        mark(3)
         out = ops.rows_topk(F, k, Ad.by_user, True, deu, dei)
-        mark(5)
+        mark(4)
         return out
     dense()
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     t0 = time.perf_counter()
     dense(ev)
     torch.cuda.synchronize()
     dd = time.perf_counter() - t0
-    ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(5)]
+    ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]
     I2 = 8.0 * di * di
     kern = {
-        "lg_spread_general_f64": (ms[1], I2),
-        "lg_hybrid_weight_f64": (ms[2], 2 * I2),
-        "lg_spread_resource_f64": (ms[3], 8.0 * de * di + 8.0 * du * di),
-        "lg_rows_topk_f64": (ms[4], 8.0 * du * di),
+        "lg_spread_hybrid_f64": (ms[1], I2),
+        "lg_spread_resource_f64": (ms[2], 8.0 * de * di + 8.0 * du * di),
+        "lg_rows_topk_f64": (ms[3], 8.0 * du * di),
     }
     roof = {n: {"ms": t, "alg_bytes": b, "achieved_GBs": b / t / 1e6,
                 "frac": b / t / 1e6 / HBM_PEAK_GBS} for n, (t, b) in kern.items()}
     return {"users": du, "items": di, "interactions": de, "seconds": dd, "recs_per_s": du / dd,
             "kernels": roof, "setup_ms": ms[0],
-            "path": "lg_spread_general_f64 + lg_hybrid_weight_f64 + lg_spread_resource_f64 + "
-                    "lg_rows_topk_f64"}
+            "path": "lg_spread_hybrid_f64 + lg_spread_resource_f64 + lg_rows_topk_f64"}
 
 
 def bench_topk(e0_orig, keys, U, I, D, k, nu, rank, world, dev):

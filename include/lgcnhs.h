@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 13
+#define LG_ABI_VERSION 14
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -190,6 +190,16 @@ int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *item_users,
                           const int64_t *user_rowptr, const int32_t *user_items,
                           int64_t n_users, int64_t n_items, double *gW,
                           lg_stream_t stream);
+
+/* W = lg_hybrid_weight_f64(lg_spread_general_f64(...), k_item, lambda, either transpose)
+ * bit for bit, without general_W in memory (general_W is exactly symmetric): getSpreading-
+ * GeneralMat + HybridS (model/SpreadMethod/model.py:14-27, 63-85) for one lambda. W is
+ * [n_items, n_items], fully written; ws: lg_spread_hybrid_ws_bytes(n_items) bytes. */
+size_t lg_spread_hybrid_ws_bytes(int64_t n_items);
+int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                         const int64_t *user_rowptr, const int32_t *user_items,
+                         const double *k_item, int64_t n_users, int64_t n_items, double lambda,
+                         double *W, void *ws, size_t ws_bytes, lg_stream_t stream);
 
 /* W[i][j] = gWsrc[i][j] / den, den = k_i^(1-lambda) * k_j^lambda, den == 0 -> 1, with
  * gWsrc = gW (transpose_gw = 0) or gW^T (transpose_gw = 1). HybridS,

@@ -38,6 +38,85 @@ __global__ __launch_bounds__(256) void k_spread_general(
   }
 }
 
+// The two factors of HybridS's denominator per item: alpha = k^(1-l), beta = k^l (the pow()
+// calls of k_hybrid_weight).
+__global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict__ k_item,
+                                                        int64_t n, double lambda,
+                                                        double *__restrict__ alpha,
+                                                        double *__restrict__ beta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  alpha[i] = pow(k_item[i], 1.0 - lambda);
+  beta[i] = pow(k_item[i], lambda);
+}
+
+// general_W and HybridS in one pass, W = general_W / den without general_W in memory: one
+// block per item row i, the row built kSpreadCols columns at a time in an LDS accumulator
+// (the same fp64 adds in the same order as k_spread_general: users of i ascending, one
+// fl(1/k_v) per item of v in the column range), then written as fl(acc / fl(alpha_i beta_j))
+// (den == 0 -> 1), k_hybrid_weight's arithmetic. general_W is exactly symmetric, so its
+// transposed form gives the same W. Each user's position in its sorted item row is carried
+// from one column range to the next in LDS (the thread that meets the range's end records
+// it; a binary search per user and range cost ~7 dependent loads) for the first kSpreadUsers
+// users of the row, found by binary search beyond. At the C3 shape this writes one I x I
+// matrix instead of writing general_W, reading it back and writing W.
+constexpr int kSpreadCols = 4096;
+constexpr int kSpreadUsers = 1024;
+__global__ __launch_bounds__(256) void k_spread_hybrid(
+    const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
+    const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
+    int64_t n_items, const double *__restrict__ alpha, const double *__restrict__ beta,
+    double *__restrict__ W) {
+  __shared__ double acc[kSpreadCols];
+  __shared__ int32_t cur[kSpreadUsers];  // user e's next position, relative to its row start
+  const int64_t i = blockIdx.x;
+  double *row = W + i * n_items;
+  const double ai = alpha[i];
+  const int64_t eb = item_rowptr[i], ee = item_rowptr[i + 1];
+  for (int64_t c0 = 0; c0 < n_items; c0 += kSpreadCols) {
+    const int64_t c1 = c0 + kSpreadCols < n_items ? c0 + kSpreadCols : n_items;
+    for (int t = threadIdx.x; t < kSpreadCols; t += blockDim.x) acc[t] = 0.0;
+    __syncthreads();
+    // the next user's row bounds are loaded while this one's items are added
+    int64_t pbn = 0, pen = 0;
+    if (eb < ee) {
+      const int32_t v0 = item_users[eb];
+      pbn = user_rowptr[v0];
+      pen = user_rowptr[v0 + 1];
+    }
+    for (int64_t e = eb; e < ee; ++e) {
+      const int64_t pb = pbn, pe = pen;
+      if (e + 1 < ee) {
+        const int32_t vn = item_users[e + 1];
+        pbn = user_rowptr[vn];
+        pen = user_rowptr[vn + 1];
+      }
+      const double wv = 1.0 / (double)(pe - pb);  // k_spread_general's fl(1/k_v)
+      const int64_t eu = e - eb;
+      const bool tracked = eu < kSpreadUsers;  // (uniform)
+      const int64_t p0 = c0 == 0 ? pb
+                         : tracked ? pb + cur[eu]
+                                   : lower_bound_i32(user_items, pb, pe, (int32_t)c0);
+      for (int64_t p = p0 + threadIdx.x; p < pe; p += blockDim.x) {
+        const int32_t j = user_items[p];
+        if (j >= c1) {  // (ascending: this thread's later items are past the range too)
+          if (tracked && (p == p0 || user_items[p - 1] < c1)) cur[eu] = (int32_t)(p - pb);
+          break;
+        }
+        acc[j - c0] += wv;
+        if (tracked && p == pe - 1) cur[eu] = (int32_t)(pe - pb);
+      }
+      __syncthreads();  // the next user may hit the same columns from other threads
+    }
+    for (int64_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
+      double den = ai * beta[j];
+      if (den == 0.0) den = 1.0;
+      row[j] = acc[j - c0] / den;
+    }
+    __syncthreads();  // (acc is zeroed for the next range)
+  }
+}
+
 // 32x32 tiles; the transposed source is staged through LDS for coalesced reads. The
 // tile's 32 row factors k_i^(1-l) and 32 column factors k_j^l are computed once per tile
 // (np.power(item_degrees, 1 - Lambda) / np.power(item_degrees, Lambda)).
@@ -248,6 +327,33 @@ extern "C" int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *
   k_spread_general<<<dim3((unsigned)n_items), dim3(256), 0, (hipStream_t)stream>>>(
       item_rowptr, item_users, user_rowptr, user_items, n_items, gW);
   return launch_status("lg_spread_general_f64");
+}
+
+extern "C" size_t lg_spread_hybrid_ws_bytes(int64_t n_items) {
+  return (size_t)(n_items > 0 ? n_items : 0) * 2 * sizeof(double);
+}
+
+extern "C" int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *item_users,
+                                    const int64_t *user_rowptr, const int32_t *user_items,
+                                    const double *k_item, int64_t n_users, int64_t n_items,
+                                    double lambda, double *W, void *ws, size_t ws_bytes,
+                                    lg_stream_t stream) {
+  LG_REQUIRE(item_rowptr && user_rowptr && k_item && W && n_users >= 0 && n_items >= 0 &&
+                 n_items < 0x7fffffff,
+             "lg_spread_hybrid_f64: bad arguments");
+  if (n_items == 0) return LG_OK;
+  const size_t need = lg_spread_hybrid_ws_bytes(n_items);
+  if (!ws || ws_bytes < need) {
+    set_error("lg_spread_hybrid_f64: workspace %zu < %zu bytes", ws_bytes, need);
+    return LG_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  double *alpha = (double *)ws, *beta = alpha + n_items;
+  k_hybrid_factors<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
+      k_item, n_items, lambda, alpha, beta);
+  k_spread_hybrid<<<dim3((unsigned)n_items), dim3(256), 0, s>>>(
+      item_rowptr, item_users, user_rowptr, user_items, n_items, alpha, beta, W);
+  return launch_status("lg_spread_hybrid_f64");
 }
 
 extern "C" int lg_hybrid_weight_f64(const double *gW, const double *k_item, int64_t n_items,

@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("LGCNHS_LIB_PATH") or LIB_PATH
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -70,6 +70,9 @@ SIGNATURES = {
     ),
     "lg_spread_general_f64": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
     "lg_hybrid_weight_f64": (ctypes.c_int, [_vp, _vp, _i64, _f64, _i32, _vp, _vp]),
+    "lg_spread_hybrid_ws_bytes": (_sz, [_i64]),
+    "lg_spread_hybrid_f64": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f64, _vp, _vp,
+                                            _sz, _vp]),
     "lg_spread_resource_f64": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp]),
     "lg_rows_topk_f64": (
         ctypes.c_int,

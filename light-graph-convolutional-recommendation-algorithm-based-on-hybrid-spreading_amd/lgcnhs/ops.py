@@ -338,6 +338,21 @@ def hybrid_weight(gW: torch.Tensor, k_item: torch.Tensor, lam: float,
     return W
 
 
+def spread_hybrid(A: Interactions, lam: float) -> torch.Tensor:
+    """hybrid_weight(spread_general(A), A.k_item, lam) (either transpose: general_W is
+    exactly symmetric) bit for bit, without general_W in memory (lg_spread_hybrid_f64)."""
+    dev = A.k_item.device
+    I = A.n_items
+    W = torch.empty((I, I), dtype=torch.float64, device=dev)
+    ws = torch.empty(max(1, N.lib().lg_spread_hybrid_ws_bytes(I)), dtype=torch.uint8,
+                     device=dev)
+    N.check(N.lib().lg_spread_hybrid_f64(
+        N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.rowptr),
+        N.ptr(A.by_user.col), N.ptr(A.k_item), A.n_users, I, float(lam), N.ptr(W), N.ptr(ws),
+        ws.numel(), N.stream_handle(dev)), "lg_spread_hybrid_f64")
+    return W
+
+
 def spread_resource(A: Interactions, W: torch.Tensor, users: slice | None = None,
                     out: torch.Tensor | None = None) -> torch.Tensor:
     """F rows for users [u0, u1) (all by default)."""
@@ -1007,5 +1022,5 @@ def spread_recommend(A: Interactions, lam: float, k: int, excl: RowSets | None,
         tiled = not dense_spread_fits(A.n_items, A.k_item.device)
     if tiled:
         return spread_topk_tiled(A, lam, k, excl, drop, eu, ei)
-    W = hybrid_weight(spread_general(A), A.k_item, lam, transpose)
+    W = spread_hybrid(A, lam)  # (= hybrid_weight(spread_general(A), ..., transpose))
     return spread_topk(A, W, k, excl, drop, eu, ei)

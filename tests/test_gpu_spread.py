@@ -126,3 +126,26 @@ def test_dense_api_G_times_F_path(golden):
     recs = recommendForAllUser(G * F, U, tr, va, k)
     _, idx = spread_lightgcn_topk(m, U, I, tr, va, float(g["slgcn_lambda"]), k)
     np.testing.assert_array_equal(np.array([recs[u] for u in range(U)]), idx.cpu().numpy())
+
+
+@pytest.mark.parametrize("zipf,U,I,n", [(False, 300, 900, 9000), (True, 400, 9000, 40000),
+                                        (True, 50, 4096, 3000), (False, 20, 4097, 200)])
+def test_spread_hybrid_equals_general_then_hybrid(zipf, U, I, n):
+    """lg_spread_hybrid_f64 (general_W and HybridS in one pass, the dense recommend path)
+    writes W bit for bit as lg_spread_general_f64 -> lg_hybrid_weight_f64 does, transposed
+    or not (general_W is exactly symmetric), over several 4096-column ranges, with items no
+    user holds (k = 0: den == 0 -> 1) and at lambda 0 and 1."""
+    from lgcnhs import ops
+    rng = np.random.default_rng(U + I)
+    items = (rng.zipf(1.3, n) - 1) % I if zipf else rng.integers(0, I - I // 10, n)
+    users = rng.integers(0, U, n)
+    key = np.unique(users.astype(np.int64) * I + items)
+    A = ops.Interactions.from_pairs(torch.as_tensor(key // I), torch.as_tensor(key % I), U, I,
+                                    DEV)
+    assert bool((A.k_item == 0).any())
+    gW = ops.spread_general(A)
+    for lam in (0.0, 0.37, 1.0):
+        W = ops.spread_hybrid(A, lam)
+        for tr in (False, True):
+            ref = ops.hybrid_weight(gW, A.k_item, lam, transpose=tr)
+            assert torch.equal(W.view(torch.int64), ref.view(torch.int64)), (lam, tr)
