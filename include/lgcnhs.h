@@ -194,8 +194,8 @@ int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *item_users,
 /* W = lg_hybrid_weight_f64(lg_spread_general_f64(...), k_item, lambda, either transpose)
  * bit for bit, without general_W in memory (general_W is exactly symmetric): getSpreading-
  * GeneralMat + HybridS (model/SpreadMethod/model.py:14-27, 63-85) for one lambda. W is
- * [n_items, n_items], fully written; ws: lg_spread_hybrid_ws_bytes(n_items) bytes. */
-size_t lg_spread_hybrid_ws_bytes(int64_t n_items);
+ * [n_items, n_items], fully written; ws: lg_spread_hybrid_ws_bytes(n_items, n_users) bytes. */
+size_t lg_spread_hybrid_ws_bytes(int64_t n_items, int64_t n_users);
 int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *item_users,
                          const int64_t *user_rowptr, const int32_t *user_items,
                          const double *k_item, int64_t n_users, int64_t n_items, double lambda,

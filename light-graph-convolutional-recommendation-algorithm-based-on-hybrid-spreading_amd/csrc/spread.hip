@@ -50,70 +50,85 @@ __global__ __launch_bounds__(256) void k_hybrid_factors(const double *__restrict
   beta[i] = pow(k_item[i], lambda);
 }
 
-// general_W and HybridS in one pass, W = general_W / den without general_W in memory: one
-// block per item row i, the row built kSpreadCols columns at a time in an LDS accumulator
-// (the same fp64 adds in the same order as k_spread_general: users of i ascending, one
-// fl(1/k_v) per item of v in the column range), then written as fl(acc / fl(alpha_i beta_j))
-// (den == 0 -> 1), k_hybrid_weight's arithmetic. general_W is exactly symmetric, so its
-// transposed form gives the same W. Each user's position in its sorted item row is carried
-// from one column range to the next in LDS (the thread that meets the range's end records
-// it; a binary search per user and range cost ~7 dependent loads) for the first kSpreadUsers
-// users of the row, found by binary search beyond. At the C3 shape this writes one I x I
-// matrix instead of writing general_W, reading it back and writing W.
+// general_W and HybridS in one pass, W = general_W / den without general_W in memory. One
+// block per (item row i, range of kSpreadCols columns): the range of the row is summed in an
+// LDS accumulator with the same fp64 adds in the same order as k_spread_general (users of i
+// ascending, one fl(1/k_v) per item of v in the range), then written as
+// fl(acc / fl(alpha_i beta_j)) (den == 0 -> 1), k_hybrid_weight's arithmetic. general_W is
+// exactly symmetric, so its transposed form gives the same W. Where each user's items enter
+// each range comes from a table built once (k_user_range_starts). Users are taken kSpreadG at
+// a time: their row bounds and range starts, then every thread's item of each of them, are
+// loaded together (one round trip per kind, not one per user), and the adds follow user by
+// user (a barrier between users: two may share a column). Rows of hub items (hundreds of
+// users) spread over the ranges' blocks instead of one block's chain. At the C3 shape this
+// writes one I x I matrix instead of writing general_W, reading it back and writing W.
 constexpr int kSpreadCols = 4096;
-constexpr int kSpreadUsers = 1024;
+constexpr int kSpreadG = 8;
+
+// starts[v][r] = the position (relative to v's row) of v's first item >= r kSpreadCols, for
+// r = 0 .. n_ranges (the last: the row's length)
+__global__ __launch_bounds__(256) void k_user_range_starts(const int64_t *__restrict__ user_rowptr,
+                                                           const int32_t *__restrict__ user_items,
+                                                           int64_t n_users, int n_ranges,
+                                                           int32_t *__restrict__ starts) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n_users * (n_ranges + 1)) return;
+  const int64_t v = x / (n_ranges + 1);
+  const int r = (int)(x - v * (n_ranges + 1));
+  const int64_t pb = user_rowptr[v], pe = user_rowptr[v + 1];
+  const int64_t c = (int64_t)r * kSpreadCols;
+  const int64_t p = r == n_ranges ? pe : lower_bound_i32(user_items, pb, pe, (int32_t)(c < 0x7fffffff ? c : 0x7fffffff));
+  starts[x] = (int32_t)(p - pb);
+}
+
 __global__ __launch_bounds__(256) void k_spread_hybrid(
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
     const int64_t *__restrict__ user_rowptr, const int32_t *__restrict__ user_items,
-    int64_t n_items, const double *__restrict__ alpha, const double *__restrict__ beta,
+    const int32_t *__restrict__ starts, int n_ranges, int64_t n_items,
+    const double *__restrict__ alpha, const double *__restrict__ beta,
     double *__restrict__ W) {
   __shared__ double acc[kSpreadCols];
-  __shared__ int32_t cur[kSpreadUsers];  // user e's next position, relative to its row start
-  const int64_t i = blockIdx.x;
-  double *row = W + i * n_items;
-  const double ai = alpha[i];
+  const int64_t i = blockIdx.x / n_ranges;
+  const int r = (int)(blockIdx.x - i * n_ranges);
+  const int64_t c0 = (int64_t)r * kSpreadCols;
+  const int64_t c1 = c0 + kSpreadCols < n_items ? c0 + kSpreadCols : n_items;
+  const int tid = threadIdx.x;
+  for (int t = tid; t < kSpreadCols; t += blockDim.x) acc[t] = 0.0;
+  __syncthreads();
   const int64_t eb = item_rowptr[i], ee = item_rowptr[i + 1];
-  for (int64_t c0 = 0; c0 < n_items; c0 += kSpreadCols) {
-    const int64_t c1 = c0 + kSpreadCols < n_items ? c0 + kSpreadCols : n_items;
-    for (int t = threadIdx.x; t < kSpreadCols; t += blockDim.x) acc[t] = 0.0;
-    __syncthreads();
-    // the next user's row bounds are loaded while this one's items are added
-    int64_t pbn = 0, pen = 0;
-    if (eb < ee) {
-      const int32_t v0 = item_users[eb];
-      pbn = user_rowptr[v0];
-      pen = user_rowptr[v0 + 1];
+  for (int64_t g0 = eb; g0 < ee; g0 += kSpreadG) {
+    const int ng = ee - g0 < kSpreadG ? (int)(ee - g0) : kSpreadG;
+    int64_t pb[kSpreadG];
+    int32_t sb[kSpreadG], se[kSpreadG];
+    int32_t deg[kSpreadG];
+#pragma unroll
+    for (int g = 0; g < kSpreadG; ++g) {
+      const int32_t v = item_users[g0 + (g < ng ? g : 0)];
+      pb[g] = user_rowptr[v];
+      deg[g] = (int32_t)(user_rowptr[v + 1] - pb[g]);
+      sb[g] = starts[(int64_t)v * (n_ranges + 1) + r];
+      se[g] = starts[(int64_t)v * (n_ranges + 1) + r + 1];
     }
-    for (int64_t e = eb; e < ee; ++e) {
-      const int64_t pb = pbn, pe = pen;
-      if (e + 1 < ee) {
-        const int32_t vn = item_users[e + 1];
-        pbn = user_rowptr[vn];
-        pen = user_rowptr[vn + 1];
-      }
-      const double wv = 1.0 / (double)(pe - pb);  // k_spread_general's fl(1/k_v)
-      const int64_t eu = e - eb;
-      const bool tracked = eu < kSpreadUsers;  // (uniform)
-      const int64_t p0 = c0 == 0 ? pb
-                         : tracked ? pb + cur[eu]
-                                   : lower_bound_i32(user_items, pb, pe, (int32_t)c0);
-      for (int64_t p = p0 + threadIdx.x; p < pe; p += blockDim.x) {
-        const int32_t j = user_items[p];
-        if (j >= c1) {  // (ascending: this thread's later items are past the range too)
-          if (tracked && (p == p0 || user_items[p - 1] < c1)) cur[eu] = (int32_t)(p - pb);
-          break;
-        }
-        acc[j - c0] += wv;
-        if (tracked && p == pe - 1) cur[eu] = (int32_t)(pe - pb);
-      }
+    int32_t x[kSpreadG];  // this thread's first item of each user in the range (-1: none)
+#pragma unroll
+    for (int g = 0; g < kSpreadG; ++g)
+      x[g] = g < ng && sb[g] + tid < se[g] ? user_items[pb[g] + sb[g] + tid] : -1;
+#pragma unroll
+    for (int g = 0; g < kSpreadG; ++g) {
+      if (g >= ng) break;
+      const double wv = 1.0 / (double)deg[g];  // k_spread_general's fl(1/k_v)
+      if (x[g] >= 0) acc[x[g] - c0] += wv;
+      for (int32_t q = sb[g] + tid + (int32_t)blockDim.x; q < se[g]; q += blockDim.x)
+        acc[user_items[pb[g] + q] - c0] += wv;  // (users with > 256 items in the range)
       __syncthreads();  // the next user may hit the same columns from other threads
     }
-    for (int64_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
-      double den = ai * beta[j];
-      if (den == 0.0) den = 1.0;
-      row[j] = acc[j - c0] / den;
-    }
-    __syncthreads();  // (acc is zeroed for the next range)
+  }
+  double *row = W + i * n_items;
+  const double ai = alpha[i];
+  for (int64_t j = c0 + tid; j < c1; j += blockDim.x) {
+    double den = ai * beta[j];
+    if (den == 0.0) den = 1.0;
+    row[j] = acc[j - c0] / den;
   }
 }
 
@@ -329,8 +344,12 @@ extern "C" int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *
   return launch_status("lg_spread_general_f64");
 }
 
-extern "C" size_t lg_spread_hybrid_ws_bytes(int64_t n_items) {
-  return (size_t)(n_items > 0 ? n_items : 0) * 2 * sizeof(double);
+static int spread_ranges(int64_t n_items) { return (int)((n_items + kSpreadCols - 1) / kSpreadCols); }
+
+extern "C" size_t lg_spread_hybrid_ws_bytes(int64_t n_items, int64_t n_users) {
+  if (n_items <= 0) return 0;
+  return (size_t)n_items * 2 * sizeof(double) +
+         (size_t)(n_users > 0 ? n_users : 0) * (spread_ranges(n_items) + 1) * sizeof(int32_t);
 }
 
 extern "C" int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *item_users,
@@ -342,17 +361,25 @@ extern "C" int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *i
                  n_items < 0x7fffffff,
              "lg_spread_hybrid_f64: bad arguments");
   if (n_items == 0) return LG_OK;
-  const size_t need = lg_spread_hybrid_ws_bytes(n_items);
+  const size_t need = lg_spread_hybrid_ws_bytes(n_items, n_users);
   if (!ws || ws_bytes < need) {
     set_error("lg_spread_hybrid_f64: workspace %zu < %zu bytes", ws_bytes, need);
     return LG_ERR_WORKSPACE;
   }
+  const int nr = spread_ranges(n_items);
+  LG_REQUIRE((int64_t)nr * n_items < 0x7fffffff, "lg_spread_hybrid_f64: %lld items: too many",
+             (long long)n_items);
   hipStream_t s = (hipStream_t)stream;
   double *alpha = (double *)ws, *beta = alpha + n_items;
+  int32_t *starts = (int32_t *)(beta + n_items);
   k_hybrid_factors<<<dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, s>>>(
       k_item, n_items, lambda, alpha, beta);
-  k_spread_hybrid<<<dim3((unsigned)n_items), dim3(256), 0, s>>>(
-      item_rowptr, item_users, user_rowptr, user_items, n_items, alpha, beta, W);
+  const int64_t ns = n_users * (nr + 1);
+  if (ns > 0)
+    k_user_range_starts<<<dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s>>>(
+        user_rowptr, user_items, n_users, nr, starts);
+  k_spread_hybrid<<<dim3((unsigned)(nr * n_items)), dim3(256), 0, s>>>(
+      item_rowptr, item_users, user_rowptr, user_items, starts, nr, n_items, alpha, beta, W);
   return launch_status("lg_spread_hybrid_f64");
 }
 

@@ -70,7 +70,7 @@ SIGNATURES = {
     ),
     "lg_spread_general_f64": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
     "lg_hybrid_weight_f64": (ctypes.c_int, [_vp, _vp, _i64, _f64, _i32, _vp, _vp]),
-    "lg_spread_hybrid_ws_bytes": (_sz, [_i64]),
+    "lg_spread_hybrid_ws_bytes": (_sz, [_i64, _i64]),
     "lg_spread_hybrid_f64": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f64, _vp, _vp,
                                             _sz, _vp]),
     "lg_spread_resource_f64": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp]),

@@ -344,8 +344,8 @@ def spread_hybrid(A: Interactions, lam: float) -> torch.Tensor:
     dev = A.k_item.device
     I = A.n_items
     W = torch.empty((I, I), dtype=torch.float64, device=dev)
-    ws = torch.empty(max(1, N.lib().lg_spread_hybrid_ws_bytes(I)), dtype=torch.uint8,
-                     device=dev)
+    ws = torch.empty(max(1, N.lib().lg_spread_hybrid_ws_bytes(I, A.n_users)),
+                     dtype=torch.uint8, device=dev)
     N.check(N.lib().lg_spread_hybrid_f64(
         N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.rowptr),
         N.ptr(A.by_user.col), N.ptr(A.k_item), A.n_users, I, float(lam), N.ptr(W), N.ptr(ws),
