@@ -58,6 +58,26 @@ def test_hybrid_transpose_and_rows_topk_exact():
             ov, oi = O.rows_topk(F, k, rp, col, drop=drop)
             np.testing.assert_array_equal(i.cpu().numpy(), oi)
             np.testing.assert_array_equal(v.cpu().numpy(), ov)
+    # rows of >= 4096 columns: 8 waves per row, their lists merged (ties across the waves'
+    # column ranges: the smaller column first, as in one ascending scan)
+    F = np.round(rng.random((12, 5001)) * 4) / 4
+    F[3, :] = 0.5  # one row all ties
+    rp, col = O.exclusion_csr(12, 5001, (rng.integers(0, 12, 3000), rng.integers(0, 5001, 3000)))
+    ex = RowSets(torch.as_tensor(rp).to(DEV), torch.as_tensor(col).to(DEV), 12, 5001)
+    for k in (1, 20, 64, 100, 128):
+        v, i = ops.rows_topk(torch.as_tensor(F).to(DEV), k, ex, drop=True)
+        ov, oi = O.rows_topk(F, k, rp, col, drop=True)
+        np.testing.assert_array_equal(i.cpu().numpy(), oi)
+        np.testing.assert_array_equal(v.cpu().numpy(), ov)
+    # and with the G factor: the fp32 chain score (oracle/score_chain.c) times F, in fp64
+    eu = (rng.standard_normal((12, 64)) * 0.1).astype(np.float32)
+    ei = (rng.standard_normal((5001, 64)) * 0.1).astype(np.float32)
+    GF = O.chain_scores(eu, ei).astype(np.float64) * F
+    v, i = ops.rows_topk(torch.as_tensor(F).to(DEV), 20, ex, drop=True,
+                         eu=torch.as_tensor(eu).to(DEV), ei=torch.as_tensor(ei).to(DEV))
+    ov, oi = O.rows_topk(GF, 20, rp, col, drop=True)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(v.cpu().numpy(), ov)
 
 
 @pytest.mark.parametrize("tag", ["hybrid", "hybrid85", "probs_ml", "heats_db"])
