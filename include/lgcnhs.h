@@ -156,11 +156,12 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
  *   umarg[u] >= (||du|| I + (||eu[u]|| + ||du||) DI + (2.01 dim 2^-24 + 2^-22) ||eu[u]|| I)
  * with du = eu[u] - bf16(eu[u]), I = max_i ||ei[i]||, DI = max_i ||ei[i] - bf16(ei[i])||
  * (lgcnhs.ops.screen_margins, from lg_bound_prep_f32's norm_up / err_up; the round-3 form
- * 0.0081 ||eu[u]|| I is larger and also valid). Every umarg[u] must be finite (so every
- * embedding is finite and no product overflows): lgcnhs.ops routes other inputs to
- * lg_score_topk_f32. One pass keeps per user the items whose bound can still reach the k-th
+ * 0.0081 ||eu[u]|| I is larger and also valid). Any input is memory-safe and gives
+ * lg_score_topk_f32's lists: a umarg[u] that is NaN, negative or +inf (non-finite
+ * embeddings), and any NaN bf16 product, is no bound -- those items enter the user's list
+ * and get the exact chain (NaN chain scores never rank, as in lg_score_topk_f32). One pass keeps per user the items whose bound can still reach the k-th
  * largest lower bound, and ranks those by the exact chain at the end (every k <= 128).
- * Workspace and splits as lg_score_topk_f32. For k <= 32 on catalogs of >= 1024 k items a
+ * Workspace and splits as lg_score_topk_f32. On catalogs of >= 1024 k items a
  * screen-only seed pass over the first 1/16 of the items runs first and leaves each user's
  * starting threshold in out_val[u * k + k - 1] (overwritten by the result); the outputs do
  * not depend on it. */

@@ -336,7 +336,8 @@ extern "C" int lg_spread_general_f64(const int64_t *item_rowptr, const int32_t *
                                      const int64_t *user_rowptr, const int32_t *user_items,
                                      int64_t n_users, int64_t n_items, double *gW,
                                      lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_rowptr && gW && n_users >= 0 && n_items >= 0,
+  LG_REQUIRE(item_rowptr && item_users && user_rowptr && user_items && gW && n_users >= 0 &&
+                 n_items >= 0,
              "lg_spread_general_f64: bad arguments");
   if (n_items == 0) return LG_OK;
   k_spread_general<<<dim3((unsigned)n_items), dim3(256), 0, (hipStream_t)stream>>>(
@@ -357,8 +358,8 @@ extern "C" int lg_spread_hybrid_f64(const int64_t *item_rowptr, const int32_t *i
                                     const double *k_item, int64_t n_users, int64_t n_items,
                                     double lambda, double *W, void *ws, size_t ws_bytes,
                                     lg_stream_t stream) {
-  LG_REQUIRE(item_rowptr && user_rowptr && k_item && W && n_users >= 0 && n_items >= 0 &&
-                 n_items < 0x7fffffff,
+  LG_REQUIRE(item_rowptr && item_users && user_rowptr && user_items && k_item && W &&
+                 n_users >= 0 && n_items >= 0 && n_items < 0x7fffffff,
              "lg_spread_hybrid_f64: bad arguments");
   if (n_items == 0) return LG_OK;
   const size_t need = lg_spread_hybrid_ws_bytes(n_items, n_users);
@@ -398,7 +399,8 @@ extern "C" int lg_hybrid_weight_f64(const double *gW, const double *k_item, int6
 extern "C" int lg_spread_resource_f64(const int64_t *user_rowptr, const int32_t *user_items,
                                       const double *W, int64_t n_users, int64_t n_items,
                                       double *F, int64_t ldf, lg_stream_t stream) {
-  LG_REQUIRE(user_rowptr && W && F && n_users >= 0 && n_items >= 0 && ldf >= n_items,
+  LG_REQUIRE(user_rowptr && user_items && W && F && n_users >= 0 && n_items >= 0 &&
+                 ldf >= n_items,
              "lg_spread_resource_f64: bad arguments");
   if (n_users == 0 || n_items == 0) return LG_OK;
   hipStream_t s = (hipStream_t)stream;

@@ -541,7 +541,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
     for (int s = 0; s < S; ++s)
       ub[g][s] = *reinterpret_cast<const bf16x8 *>(eub + uu * D + 32 * s + 8 * gq);
-    marg[g] = umarg[uu];
+    // A margin that is no bound (NaN, negative) becomes NaN: every bound of that user is NaN
+    // and enters (the compares below are !(bound <= thr)), so the user's items all get the
+    // exact chain -- k_score_topk's lists for any input. (+inf works as it is: every bound is
+    // +inf or NaN.) Padding users take 0: their thr = +inf keeps them out of every list unless
+    // a product itself is NaN (then the entry is harmless: exact_entries clamps the user and
+    // padding lists are never written out).
+    {
+      const float mr = umarg[uu];
+      marg[g] = !uvalid[g] ? 0.f : (mr >= 0.f ? mr : __builtin_nanf(""));
+    }
     ex_pos[g] = 0;
     ex_hi[g] = 0;
     if (ex_rowptr && uvalid[g]) {
@@ -802,9 +811,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const int rel = t * 16 + gq * 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      // (the margins are finite -- the caller's contract -- so a bound compares as a number:
-      // padding users past n_users, thr = +inf, never enter)
-      const bool cand = rel + r < n_valid && acc[r] + marg[g] > thr[g];
+      // (a NaN bound -- a NaN product or margin -- enters: its exact chain decides)
+      const bool cand = rel + r < n_valid && above(acc[r] + marg[g], thr[g]);
       const uint64_t bal = __ballot(cand);
       LG_COUNT(0, __popcll(bal));
       if (bal) {
@@ -937,8 +945,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     // The chunk's test: per group the largest product of the chunk plus the margin against
     // the threshold, one ballot per group; returns the groups (bits) with a possible entrant.
     // Tests run against the thresholds of that moment: never above the later ones (they only
-    // rise). (Finite margins and embeddings, the caller's contract: a bound is a number; a
-    // NaN product -- never an exact score that enters -- would not hit.)
+    // rise). The maxima propagate NaN (v_maximum3), and !(bound <= thr) hits on a NaN bound: a
+    // NaN product or margin sends its tile down the insertion path, where the item's own bound
+    // decides (the same compare) and its exact chain ranks it.
     auto test_chunk = [&](const Accs &acc) __attribute__((always_inline)) {
       uint32_t gm = 0;
 #pragma unroll
@@ -950,13 +959,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
               m, __builtin_elementwise_maximum(
                      __builtin_elementwise_maximum(acc[tt][g][0], acc[tt][g][1]),
                      __builtin_elementwise_maximum(acc[tt][g][2], acc[tt][g][3])));
-        if (__ballot(m + marg[g] > thr[g]) != 0) gm |= 1u << g;
+        if (__ballot(above(m + marg[g], thr[g])) != 0) gm |= 1u << g;
       }
       return gm;
     };
     // the seed pass: each lane's R largest lower bounds per class (past the range: -inf),
     // class (item mod NCLS) = 16 (tt mod TPC_S) + 4 gq + r; a value enters the class's sorted
-    // R slots by a max / min chain (finite margins and embeddings: the caller's contract)
+    // R slots by a max / min chain. A NaN lower bound (NaN product or margin) is no candidate:
+    // fmaxf skips it for R = 1; for R > 1 it is made -inf first (the min of the chain would
+    // otherwise carry the slot's value down as a duplicate candidate)
     auto seed_chunk = [&](int c, const Accs &acc) __attribute__((always_inline)) {
       const int t0 = c * TPC;
 #pragma unroll
@@ -967,6 +978,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = rel + r < n_valid ? lbound(acc[tt][g][r], marg[g]) : neg_inf<float>();
+            if (R > 1) v = v == v ? v : neg_inf<float>();
 #pragma unroll
             for (int l = 0; l < R; ++l) {
               const float h = cmax[g][tt % TPC_S][l][r];
@@ -989,7 +1001,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       for (int tt = 0; tt < TPC; ++tt)
 #pragma unroll
         for (int g = 0; g < NG; ++g)
-          if (((gm >> g) & 1u) && __ballot(max4(acc[tt][g]) + marg[g] > thr[g]) != 0)
+          if (((gm >> g) & 1u) && __ballot(above(max4(acc[tt][g]) + marg[g], thr[g])) != 0)
             hits |= 1u << (tt * NG + g);
       if (t0 + TPC > n_t) hits &= (1u << ((n_t - t0) * NG)) - 1u;  // (tiles past the split)
       int tt0 = 0;

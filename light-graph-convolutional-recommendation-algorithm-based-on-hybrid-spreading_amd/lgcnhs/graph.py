@@ -188,6 +188,9 @@ class RowSets:
     """Sorted, de-duplicated column sets per row: (rowptr int64 [n_rows+1], col int32)."""
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_rows: int, n_cols: int):
+        if col.numel() == 0 and col.data_ptr() == 0:
+            # an empty set still passes a valid device pointer: the C ABI refuses NULL columns
+            col = torch.empty(1, dtype=col.dtype, device=col.device)[:0]
         self.rowptr, self.col = rowptr, col
         self.n_rows, self.n_cols = int(n_rows), int(n_cols)
 

@@ -224,7 +224,7 @@ def screen_margins(un: torch.Tensor, ue: torch.Tensor, inorm: torch.Tensor,
     rounded up to fp32. On N(0, 0.1^2) embeddings this is ~0.45x the worst-case 0.0081 ||u|| I
     of SCREEN_MARGIN (bf16 rounding errors are not all at their maximum), and the observed
     error stays below 0.37 of it. Non-finite norms give non-finite margins: the kernel then
-    keeps every item of those users."""
+    ranks every item of those users by the exact chain."""
     I = inorm.max().double()
     DI = ierr.max().double()
     u, e = un.double(), ue.double()
@@ -263,12 +263,9 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     if screen and nu > 0:
         ub, un, ue = bound_operands(eu, with_err=True)
         ib, inorm, ierr = bound_operands(ei, with_err=True)
+        # (no host sync: a non-finite embedding gives non-finite margins, and the kernel then
+        # ranks those users' items by the exact chain -- include/lgcnhs.h)
         umarg = screen_margins(un, ue, inorm, ierr, d)
-        if not bool(torch.isfinite(umarg).all()):
-            # a non-finite (or overflowing) embedding makes the margins non-finite: the screen's
-            # bounds are then no numbers, and the plain kernel (the same lists by definition)
-            # ranks every item -- lg_score_topk_screened_f32's contract (include/lgcnhs.h)
-            return score_topk(eu, ei, k, excl, mask_value, n_splits, screen=False)
         N.check(N.lib().lg_score_topk_screened_f32(
             N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d, ex_rp, ex_c,
             float(mask_value), int(k), ns, N.ptr(val), N.ptr(idx), N.ptr(ws), ws_bytes,
@@ -415,6 +412,7 @@ INV_TAB = 512      # degree classes cached in LDS by the walk (csrc/spread_tiled
 MAX_CLASSES = 0x7FFF   # P slot words keep bit 31 clear (it marks V entries)
 LINE_SLOTS, LINE_ENTS = 31, 7   # P slots / V entries in a row's 128-byte line
 GROUP_MAX, GROUP_WIDE = 16, 8   # tiles per group build (tiles wider than 4096: 8)
+OVF_UNITS_MAX = 1 << 29  # a group's overflow units (the rows' 29-bit overflow pointers)
 
 
 def hybrid_recip(k_item: torch.Tensor, lam: float):
@@ -500,6 +498,7 @@ class TileWeights:
             vthr = self.tile
         self.vthr = max(LINE_SLOTS, int(vthr))
         gmax = GROUP_MAX if self.tile <= 4096 else GROUP_WIDE
+        self._auto_group = group is None  # (a default group halves itself when too large)
         if group is None:
             group = gmax
         if not 1 <= group <= gmax:
@@ -664,7 +663,13 @@ class TileWeights:
             ends = [0] * nt
         bases = [0] + ends[:-1]
         totals = [e - b for e, b in zip(ends, bases)]
-        if ends[-1] + 64 >= 1 << 29:
+        if ends[-1] + 64 >= OVF_UNITS_MAX:
+            if self._auto_group and nt > 1:
+                # the default group size: retry this group (and build the later ones) with
+                # half as many tiles -- the cursor kernel reads cur and rewrites only end
+                self.group = nt // 2
+                self._build_group(j0, stop, widths[:self.group])
+                return
             raise ValueError("tile group too large for the 29-bit overflow pointers (use a "
                              "smaller tile or group)")
         self._grow_ovf(ends[-1])

@@ -182,7 +182,8 @@ _C = None
 def _clib():
     global _C
     if _C is None:
-        path = os.path.join(HERE, "build", "liboracle.so")
+        # (ORACLE_LIB_PATH: the host-sanitized build of the sanitizer leg, oracle/Makefile asan)
+        path = os.environ.get("ORACLE_LIB_PATH") or os.path.join(HERE, "build", "liboracle.so")
         if not os.path.exists(path):
             import subprocess
             subprocess.run(["make", "-C", HERE], check=True, capture_output=True)

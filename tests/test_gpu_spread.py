@@ -148,18 +148,32 @@ def test_dense_api_G_times_F_path(golden):
     np.testing.assert_array_equal(np.array([recs[u] for u in range(U)]), idx.cpu().numpy())
 
 
-@pytest.mark.parametrize("zipf,U,I,n", [(False, 300, 900, 9000), (True, 400, 9000, 40000),
-                                        (True, 50, 4096, 3000), (False, 20, 4097, 200)])
-def test_spread_hybrid_equals_general_then_hybrid(zipf, U, I, n):
+@pytest.mark.parametrize("zipf,U,I,n,heavy", [(False, 300, 900, 9000, 0),
+                                              (True, 400, 9000, 40000, 0),
+                                              (True, 50, 4096, 3000, 0), (False, 20, 4097, 200, 0),
+                                              (False, 200, 9000, 20000, 3)])
+def test_spread_hybrid_equals_general_then_hybrid(zipf, U, I, n, heavy):
     """lg_spread_hybrid_f64 (general_W and HybridS in one pass, the dense recommend path)
     writes W bit for bit as lg_spread_general_f64 -> lg_hybrid_weight_f64 does, transposed
     or not (general_W is exactly symmetric), over several 4096-column ranges, with items no
-    user holds (k = 0: den == 0 -> 1) and at lambda 0 and 1."""
+    user holds (k = 0: den == 0 -> 1) and at lambda 0 and 1. `heavy` users hold more than 256
+    items inside one 4096-column range (Douban-style heavy users: k_spread_hybrid's strided
+    loop past the block's 256 threads): 300, 1000 and 3000 items of range 0 and 700 of
+    range 1."""
     from lgcnhs import ops
     rng = np.random.default_rng(U + I)
     items = (rng.zipf(1.3, n) - 1) % I if zipf else rng.integers(0, I - I // 10, n)
     users = rng.integers(0, U, n)
+    for h, cnt in enumerate((300, 1000, 3000)[:heavy]):
+        users = np.concatenate([users, np.full(cnt, h)])
+        items = np.concatenate([items, rng.choice(4096, cnt, replace=False)])
+    if heavy:
+        users = np.concatenate([users, np.full(700, 0)])
+        items = np.concatenate([items, 4096 + rng.choice(4096, 700, replace=False)])
     key = np.unique(users.astype(np.int64) * I + items)
+    if heavy:  # the strided loop is reached: some user has > 256 items in one range
+        ku, ki = key // I, key % I
+        assert max(int(((ku == h) & (ki < 4096)).sum()) for h in range(heavy)) > 256
     A = ops.Interactions.from_pairs(torch.as_tensor(key // I), torch.as_tensor(key % I), U, I,
                                     DEV)
     assert bool((A.k_item == 0).any())

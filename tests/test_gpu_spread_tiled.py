@@ -104,6 +104,38 @@ def test_group_build_equals_per_tile(zipf, tile, group, vthr):
         assert hub_seen
 
 
+def test_group_build_halves_default_group_on_overflow(monkeypatch):
+    """A default-size group whose overflow units pass the 29-bit pointer limit is rebuilt
+    with half as many tiles (16 -> 8 -> ...) instead of raising; its tiles are the per-tile
+    build's bit for bit. An explicit group still raises. (The limit is lowered to a few
+    hundred units so a small Zipf graph reaches it.)"""
+    from lgcnhs import ops
+    U, I, tile = 700, 900, 64
+    A = _inter(U, I, 30000, seed=5, zipf=True)
+    a = RP.PerTileWeights(A, 0.5, tile, vthr=8)
+    sizes = []
+    for j0 in range(0, I, tile):
+        a.build(j0)
+        sizes.append(a.n_units)
+    # a limit every pair of tiles fits under and the first 16 tiles do not
+    lim = max(sizes[t] + sizes[t + 1] for t in range(len(sizes) - 1)) + 65
+    assert sum(sizes[:16]) + 64 >= lim
+    monkeypatch.setattr(ops, "OVF_UNITS_MAX", lim)
+    b = ops.TileWeights(A, 0.5, tile, vthr=8)
+    assert b.group == 16 or b.group == -(-I // tile)
+    for j0 in range(0, I, tile):
+        a.build(j0)
+        b.build(j0)
+        assert (a.j0, a.width, a.n_units) == (b.j0, b.width, b.n_units)
+        assert torch.equal(a.lines, b.lines)
+        assert torch.equal(a.bound, b.bound) and torch.equal(a.row_len, b.row_len)
+        assert np.array_equal(a.dense().view(np.uint64), b.dense().view(np.uint64))
+    assert b.group < 16
+    c = ops.TileWeights(A, 0.5, tile, vthr=8, group=16)
+    with pytest.raises(ValueError, match="29-bit"):
+        c.build(0)
+
+
 @pytest.mark.parametrize("k", [1, 10, 33, 100])
 @pytest.mark.parametrize("tile", [64, 333, 4096])
 @pytest.mark.parametrize("mode", ["G_drop", "drop", "none"])

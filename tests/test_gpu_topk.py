@@ -95,37 +95,92 @@ def test_screened_topk_near_ties_and_wide_norms(k):
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
-@pytest.mark.parametrize("I", [3000, 40000])
-def test_screened_topk_non_finite_rows(I):
-    """A NaN item row makes every user's screen margin NaN and a NaN user row its own: the
-    screened path then hands the call to the plain kernel (non-finite margins are outside the
-    screened kernel's contract), so the lists stay the plain kernel's bit for bit (NaN scores
-    never enter), and finite items still fill them."""
+def _screened_direct(eu, ei, k, ex, umarg, n_splits=1):
+    """lg_score_topk_screened_f32 through the C ABI with caller-chosen margins (no host
+    routing of any kind between the inputs and the kernel)."""
+    from lgcnhs import _native as N
     from lgcnhs import ops
-    U, d, k = 64, 64, 20
+    nu, d = eu.shape
+    ni = ei.shape[0]
+    ub, _ = ops.bound_operands(eu)
+    ib, _ = ops.bound_operands(ei)
+    ws_bytes = N.lib().lg_score_topk_ws_bytes(nu, ni, d, k, n_splits)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
+    val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)
+    idx = torch.empty((nu, k), dtype=torch.int64, device=eu.device)
+    N.check(N.lib().lg_score_topk_screened_f32(
+        N.ptr(eu), N.ptr(ei), N.ptr(ub), N.ptr(ib), N.ptr(umarg), nu, ni, d,
+        N.ptr(ex.rowptr), N.ptr(ex.col), float(O.MASK), int(k), int(n_splits), N.ptr(val),
+        N.ptr(idx), N.ptr(ws), ws_bytes, N.stream_handle(eu.device)),
+        "lg_score_topk_screened_f32")
+    return val, idx
+
+
+@pytest.mark.parametrize("I,k", [(3000, 20), (40000, 20), (70000, 64), (3000, 100),
+                                 (120000, 100)])
+def test_screened_topk_non_finite_rows(I, k):
+    """lg_score_topk_screened_f32 on non-finite inputs, called directly: a NaN item row, an item
+    with an +inf element, a NaN user row, a user with a -inf element, under three margin sets --
+    the host's (every margin NaN: the item norms are), the margins of the finite inputs (NaN
+    and infinite products under finite margins), and those with NaN / negative / +inf margins
+    forced on users with finite rows. Every item of a no-bound user and every NaN-bound item
+    enters and gets the exact chain, so the lists equal lg_score_topk_f32's bit for bit (NaN
+    scores never rank), on one split and on several, with and without the seed pass (40,000
+    items and more). 70 users: the last block has padding users, whose clamped rows are NaN."""
+    from lgcnhs import ops
+    U, d = 70, 64
     eu, ei = _emb(U, d, 41), _emb(I, d, 42)
+    clean_u, clean_i = eu.clone(), ei.clone()
     ei[1234] = float("nan")
+    ei[2000, 5] = float("inf")
     eu[7] = float("nan")
+    eu[11, 3] = -float("inf")
+    eu[U - 1] = float("nan")  # the row padding users clamp to
     rp, col = _excl(U, I, 0.01, 43)
     ex = _rowsets(rp, col, U, I)
-    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, screen=True)
-    v0, i0 = ops.score_topk(eu.to(DEV), ei.to(DEV), k, ex, screen=False)
-    assert torch.equal(i, i0) and torch.equal(v.view(torch.int32), v0.view(torch.int32))
-    i = i.cpu().numpy()
-    assert (i[np.arange(U) != 7] >= 0).all() and not (i == 1234).any()
+    eu, ei = eu.to(DEV), ei.to(DEV)
+    v0, i0 = ops.score_topk(eu, ei, k, ex, n_splits=1, screen=False)
+    _, un, ue = ops.bound_operands(eu, with_err=True)
+    _, inorm, ierr = ops.bound_operands(ei, with_err=True)
+    host = ops.screen_margins(un, ue, inorm, ierr, d)
+    assert torch.isnan(host).all()
+    _, cun, cue = ops.bound_operands(clean_u.to(DEV), with_err=True)
+    _, cin, cie = ops.bound_operands(clean_i.to(DEV), with_err=True)
+    clean = ops.screen_margins(cun, cue, cin, cie, d)
+    assert torch.isfinite(clean).all()
+    forced = clean.clone()
+    forced[3], forced[4], forced[5] = float("nan"), -1.0, float("inf")
+    for name, m in (("host", host), ("clean", clean), ("forced", forced)):
+        for ns in (1, 3):
+            v, i = _screened_direct(eu, ei, k, ex, m, n_splits=ns)
+            assert torch.equal(i, i0), (name, ns)
+            assert torch.equal(v.view(torch.int32), v0.view(torch.int32)), (name, ns)
+    i0 = i0.cpu().numpy()
+    ok = np.ones(U, bool)
+    ok[[7, 11, U - 1]] = False
+    assert (i0[ok] >= 0).all() and not (i0 == 1234).any()
+    # the +inf item ranks first wherever its chain is +inf
+    assert (i0[:, 0] == 2000).sum() > 0
+    # the product path: ops.score_topk's screened default on the same inputs, no host sync
+    v, i = ops.score_topk(eu, ei, k, ex, screen=True)
+    assert np.array_equal(i.cpu().numpy(), i0)
 
 
-@pytest.mark.parametrize("k", [1, 20, 32, 64, 100])
-def test_seeded_topk_exclusions_in_seed_range(k):
+@pytest.mark.parametrize("d,k", [(64, 1), (64, 20), (64, 32), (64, 64), (64, 100), (64, 128),
+                                 (32, 20), (32, 64), (32, 128), (128, 20), (128, 32),
+                                 (128, 64), (128, 100), (128, 128)])
+def test_seeded_topk_exclusions_in_seed_range(d, k):
     """The screened kernel's seed pass (catalogs of >= 1024 k items): every user's threshold
     starts at the (k + E)-th largest of the lower bounds kept per item class over the first
     1/16 of the items (the class maximum for k <= 32, the 4 largest per class above), E = its
     excluded items there. Users whose best items of that range are excluded (E from 0 to 60:
     the seed must skip them, and there is none once k + E exceeds the candidates), items tied
     in bf16 and exactly inside the range, a zero user, users scaled over 1e-2..1e2: the lists
-    equal the plain kernel's and the C oracle's bit for bit."""
+    equal the plain kernel's and the C oracle's bit for bit. Every seed shape: d = 32 / 64
+    (64 classes: R = 1 for k <= 32, 4 above) and d = 128 (32 classes: R = 2 for k <= 32,
+    4 above through its own k <= 128 launch)."""
     from lgcnhs import ops
-    U, d = 200, 64
+    U = 200
     I = 65536 if k <= 64 else 131072
     eu, ei = _emb(U, d, 51 + k), _emb(I, d, 52)
     ei[100:140] = ei[60:100]  # exact ties inside the seed range
@@ -173,12 +228,14 @@ def test_score_topk_edge_cases():
                                                                   None, None, 3)[1])
 
 
-@pytest.mark.parametrize("k", [20, 100])
-def test_score_topk_large_catalog_sample(k):
-    """1M-item catalog (the C5 item count), 256 users: bit-exact vs the C oracle."""
+@pytest.mark.parametrize("d,k", [(64, 20), (64, 100), (32, 20), (32, 128), (128, 20),
+                                 (128, 100), (128, 128)])
+def test_score_topk_large_catalog_sample(d, k):
+    """1M-item catalog (the C5 item count), 256 users: bit-exact vs the C oracle (seeded
+    screened kernel, every width and list size)."""
     from lgcnhs import ops
     U, I = 256, 1_000_000
-    eu, ei = _emb(U, 64, 7), _emb(I, 64, 8)
+    eu, ei = _emb(U, d, 7), _emb(I, d, 8)
     rp, col = _excl(U, I, 1e-4, 9)
     ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
     v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))

@@ -81,6 +81,15 @@ def test_argument_validation_without_gpu():
     # the chunk-bound kernel's per-chunk norm table holds 64 chunks: wider tiles are refused
     st = lib.lg_score_chunk_bound(one, one, 10, one, one, 64, 0, 4097, one, z, 0, z)
     assert st == 1 and b"width 4097 > 4096" in lib.lg_last_error()
+    # the dense spreading entries dereference their column arrays: NULL is refused, not faulted
+    st = lib.lg_spread_hybrid_f64(one, z, one, one, one, 4, 4, 0.5, one, one, 1 << 20, z)
+    assert st == 1 and b"lg_spread_hybrid_f64" in lib.lg_last_error()
+    st = lib.lg_spread_hybrid_f64(one, one, one, z, one, 4, 4, 0.5, one, one, 1 << 20, z)
+    assert st == 1
+    st = lib.lg_spread_general_f64(one, z, one, one, 4, 4, one, z)
+    assert st == 1 and b"lg_spread_general_f64" in lib.lg_last_error()
+    st = lib.lg_spread_resource_f64(one, z, one, 4, 4, one, 4, z)
+    assert st == 1 and b"lg_spread_resource_f64" in lib.lg_last_error()
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 1) == 0
     assert lib.lg_score_topk_ws_bytes(100, 1000, 64, 10, 4) == 4 * 100 * 10 * 8
     # catalogs of more than 2^20 items: the screened kernel's splits (16-bit tile indices)
