@@ -430,8 +430,10 @@ def bench_small_config(dev, k):
 def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024):
     """SURVEY.md §8 f2 on the north_star graph, one GPU: the reference's training step
     (model/LightGCN/train.py:26-59,148-151; loss.py:12-70) through the package's own path:
-    HIP forward (ops.propagate), a 1024-triple mini-batch of the interactions with
-    structured negatives (model.LightGCN.loss.sampleMiniBatch), BPRLoss, backward (the
+    a 1024-triple mini-batch of the interactions with structured negatives
+    (model.LightGCN.loss.sampleMiniBatch), the HIP forward at the batch's rows
+    (ops.propagate_rows: output-restricted layers, bitwise the full forward's rows), BPRLoss,
+    backward (the
     HIP propagation with A_hat^T = A_hat) and one Adam step over all U+I embedding rows.
     The interactions here are the train|val positives the other phases exclude."""
     from lgcnhs import ops
@@ -444,9 +446,12 @@ def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024
     gen = torch.Generator(device=dev).manual_seed(42)
 
     def step():
-        out = ops.propagate(adj, e0, L)
+        # (model/LightGCN/train.py getEmbeddingForBPR: the batch first, then the forward's
+        # layers only where the batch's rows depend on them)
         u, p, n = sampleMiniBatch(batch, r_edge, I, generator=gen)
-        loss = BPRLoss(out[u], e0[u], out[U + p], e0[U + p], out[U + n], e0[U + n], 1e-6)
+        f = ops.propagate_rows(adj, e0, L, torch.cat([u, U + p, U + n]))
+        fu, fp, fn = torch.split(f, [batch, batch, batch])
+        loss = BPRLoss(fu, e0[u], fp, e0[U + p], fn, e0[U + n], 1e-6)
         opt.zero_grad()
         loss.backward()
         opt.step()
@@ -461,8 +466,10 @@ def bench_train(rowptr, src, keys, U, I, e0_orig, D, L, dev, steps=3, batch=1024
     dt = (time.perf_counter() - t0) / steps
     res = {"ms_per_step": dt * 1e3, "steps_per_s": 1.0 / dt, "batch": batch,
            "interactions_sampled": int(keys.numel()), "loss": float(loss.item()),
-           "what": "HIP forward + mini-batch with structured negatives over all interactions + "
-                   "BPR + HIP backward + Adam over all embedding rows"}
+           "what": "mini-batch with structured negatives over all interactions + HIP forward "
+                   "restricted to the rows the batch depends on (layer 3 at the batch, layer 2 "
+                   "at it and its neighbours, layer 1 in full) + BPR + HIP backward + Adam "
+                   "over all embedding rows"}
     del opt, e0, r_edge, adj
     torch.cuda.empty_cache()
     return res

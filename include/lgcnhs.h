@@ -40,7 +40,7 @@ enum lg_status {
 };
 
 /* ABI version of this header (bumped on any signature change). */
-#define LG_ABI_VERSION 14
+#define LG_ABI_VERSION 15
 int lg_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *lg_last_error(void);
@@ -127,6 +127,30 @@ int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_end,
                           const float *x0, float *acc, float *out, int32_t dim,
                           int32_t acc_mode, float denom, float *partial, lg_stream_t stream);
 
+/* Output-restricted layers (the forward of one BPR training step, reference
+ * model/LightGCN/train.py:30 `model.forward` + :31-45 indexing the mini-batch's rows: the loss
+ * reads layer L only at the batch's rows, layer L-1 only there and at their neighbours, ...):
+ * lg_spmm_layer_f32 / lg_spmm_long_rows_f32 computing only the rows r whose row_mask[r]
+ * (uint8, per node id) is non-zero; every other row of y / acc / out is left untouched. Each
+ * computed row is bitwise the unrestricted call's. lg_mark_neighbors_u8 sets out_mask[r] = 1
+ * for every row r of in_mask and every source of its entries (the rows the layer below must
+ * produce for it); out_mask is not cleared first and must not alias in_mask. */
+int lg_spmm_layer_rows_f32(const int64_t *rowptr, const int32_t *src, const float *dis,
+                           const float *w, const float *x, float *y, const float *x0,
+                           float *acc, float *out, int64_t n_rows, int64_t row_offset,
+                           int32_t dim, int32_t acc_mode, float denom, int64_t long_threshold,
+                           const uint8_t *row_mask, lg_stream_t stream);
+int lg_spmm_long_rows_masked_f32(const int64_t *seg_beg, const int64_t *seg_end,
+                                 const int32_t *seg_node, int64_t n_seg,
+                                 const int32_t *long_node, const int64_t *seg_ptr,
+                                 int64_t n_long, const int32_t *src, const float *dis,
+                                 const float *w, const float *x, float *y, const float *x0,
+                                 float *acc, float *out, int32_t dim, int32_t acc_mode,
+                                 float denom, float *partial, const uint8_t *row_mask,
+                                 lg_stream_t stream);
+int lg_mark_neighbors_u8(const int64_t *rowptr, const int32_t *src, int64_t n_rows,
+                         const uint8_t *in_mask, uint8_t *out_mask, lg_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Full-catalog scoring with exclusion mask and top-K.
  * Replaces  score = e0_u @ e0_i^T ; score[train|val positives] = -1024 ; topk(score, k)
@@ -161,10 +185,15 @@ int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users, int64_t
  * embeddings), and any NaN bf16 product, is no bound -- those items enter the user's list
  * and get the exact chain (NaN chain scores never rank, as in lg_score_topk_f32). One pass keeps per user the items whose bound can still reach the k-th
  * largest lower bound, and ranks those by the exact chain at the end (every k <= 128).
- * Workspace and splits as lg_score_topk_f32. On catalogs of >= 1024 k items a
+ * Workspace: lg_score_topk_screened_ws_bytes (the per-split partial lists as
+ * lg_score_topk_f32's, plus for k > 32 the per-user list slabs of 128 / 256 8-byte entries per
+ * split that the main pass keeps its lists in); splits as lg_score_topk_f32. On catalogs of
+ * >= 1024 k items a
  * screen-only seed pass over the first 1/16 of the items runs first and leaves each user's
  * starting threshold in out_val[u * k + k - 1] (overwritten by the result); the outputs do
  * not depend on it. */
+size_t lg_score_topk_screened_ws_bytes(int64_t n_users, int64_t n_items, int32_t dim,
+                                       int32_t k, int32_t n_splits);
 int lg_score_topk_screened_f32(const float *eu, const float *ei, const void *eu_bf16,
                                const void *ei_bf16, const float *umarg, int64_t n_users,
                                int64_t n_items, int32_t dim, const int64_t *ex_rowptr,

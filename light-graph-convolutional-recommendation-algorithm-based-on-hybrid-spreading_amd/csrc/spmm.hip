@@ -194,16 +194,83 @@ __global__ __launch_bounds__(256) void k_spmm_layer(
   epilogue<D>(g, lane % LPR, sum, y, x0, acc, out, mode, denom);
 }
 
+// Output-restricted layer (the BPR training forward: the loss reads the final embedding only
+// at the mini-batch's rows, so layer L is needed only there, layer L-1 only there and at their
+// neighbours, ...): rows whose byte in row_mask (per node) is 0 are not computed -- their y /
+// acc / out rows are left as they are. One wave per 64 consecutive rows: the lanes read the
+// rows' mask bytes and bounds, and the wave runs the marked rows one after the other through
+// the unmasked kernel's gather_sum and epilogue, so every computed row is bitwise
+// k_spmm_layer's.
+template <int D, int UNROLL>
+__global__ __launch_bounds__(256) void k_spmm_layer_rows(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ src,
+    const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
+    float *__restrict__ y, const float *__restrict__ x0, float *acc, float *out,
+    int64_t n_rows, int64_t row_offset, int mode, float denom, int64_t long_threshold,
+    const uint8_t *__restrict__ row_mask) {
+  constexpr int LPR = D / 4;
+  const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 64;
+  if (r0 >= n_rows) return;  // wave-uniform
+  const int lane = lane_id();
+  const int64_t r = r0 + lane;
+  int64_t beg = 0, end = 0;
+  bool want = false;
+  if (r < n_rows && row_mask[row_offset + r]) {
+    beg = rowptr[r];
+    end = rowptr[r + 1];
+    want = end - beg <= long_threshold;  // (longer rows: the segmented path)
+  }
+  uint64_t rows = __ballot(want);
+  while (rows) {
+    const int b = __builtin_ctzll(rows);
+    rows &= rows - 1;
+    const int64_t rb = __shfl(beg, b), re = __shfl(end, b);
+    const int64_t g = row_offset + r0 + b;
+    const float4 sum = gather_sum<D, UNROLL, false>(rb, re, src, w, dis, dis[g], x);
+    if (lane / LPR == 0) epilogue<D>(g, lane % LPR, sum, y, x0, acc, out, mode, denom);
+  }
+}
+
+// row_mask (per node): out[r] = 1 for every r with in[r] set and for every source of its
+// edges (the rows the next-lower layer must produce for it); one wave per 64 rows, each
+// marked row's edges 64 at a time. Byte stores of 1 only: concurrent duplicates are benign.
+__global__ __launch_bounds__(256) void k_mark_neighbors(const int64_t *__restrict__ rowptr,
+                                                        const int32_t *__restrict__ src,
+                                                        int64_t n_rows,
+                                                        const uint8_t *__restrict__ in,
+                                                        uint8_t *__restrict__ out) {
+  const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 64;
+  if (r0 >= n_rows) return;
+  const int lane = lane_id();
+  const int64_t r = r0 + lane;
+  int64_t beg = 0, end = 0;
+  const bool want = r < n_rows && in[r];
+  if (want) {
+    beg = rowptr[r];
+    end = rowptr[r + 1];
+    out[r] = 1;
+  }
+  uint64_t rows = __ballot(want);
+  while (rows) {
+    const int b = __builtin_ctzll(rows);
+    rows &= rows - 1;
+    const int64_t rb = __shfl(beg, b), re = __shfl(end, b);
+    for (int64_t e = rb + lane; e < re; e += 64) out[src[e]] = 1;
+  }
+}
+
 // one wave per segment: partial[s] = sum over [seg_beg[s], seg_end[s]) of w_e * x[src_e]
+// (row_mask, optional: segments of unmarked rows are skipped)
 template <int D, int UNROLL>
 __global__ __launch_bounds__(256) void k_spmm_segments(
     const int64_t *__restrict__ seg_beg, const int64_t *__restrict__ seg_end,
     const int32_t *__restrict__ seg_node, const int32_t *__restrict__ src,
     const float *__restrict__ dis, const float *__restrict__ w, const float *__restrict__ x,
-    float *__restrict__ partial, int64_t n_seg) {
+    float *__restrict__ partial, int64_t n_seg, const uint8_t *__restrict__ row_mask) {
   constexpr int LPR = D / 4;
   const int64_t sgi = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (sgi >= n_seg) return;
+  if (row_mask && !row_mask[seg_node[sgi]]) return;
   const float4 sum = gather_sum<D, UNROLL>(seg_beg[sgi], seg_end[sgi], src, w, dis,
                                            dis[seg_node[sgi]], x);
   const int lane = lane_id();
@@ -216,10 +283,12 @@ template <int D>
 __global__ __launch_bounds__(256) void k_spmm_long_reduce(
     const int32_t *__restrict__ long_node, const int64_t *__restrict__ seg_ptr,
     const float *__restrict__ partial, float *__restrict__ y, const float *__restrict__ x0,
-    float *acc, float *out, int64_t n_long, int mode, float denom) {
+    float *acc, float *out, int64_t n_long, int mode, float denom,
+    const uint8_t *__restrict__ row_mask) {
   constexpr int LPR = D / 4;
   const int64_t j = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   if (j >= n_long) return;
+  if (row_mask && !row_mask[long_node[j]]) return;
   const int lane = lane_id();
   if (lane / LPR != 0) return;  // one lane group sums the segments sequentially
   const int li = lane % LPR;
@@ -233,11 +302,17 @@ template <int D>
 static void launch_spmm(const int64_t *rowptr, const int32_t *src, const float *dis,
                         const float *w, const float *x, float *y, const float *x0, float *acc,
                         float *out, int64_t n_rows, int64_t row_offset, int mode, float denom,
-                        int64_t long_threshold, const uint8_t *live, hipStream_t stream) {
+                        int64_t long_threshold, const uint8_t *live, hipStream_t stream,
+                        const uint8_t *row_mask = nullptr) {
   constexpr int WPB = 4;  // waves (rows) per 256-thread block
   constexpr int UNROLL = (D <= 64) ? 4 : 8;
   const int64_t blocks = (n_rows + WPB - 1) / WPB;
-  if (live)
+  if (row_mask)  // (64 rows per wave)
+    k_spmm_layer_rows<D, UNROLL><<<dim3((unsigned)((n_rows + 64 * WPB - 1) / (64 * WPB))),
+                                   dim3(64 * WPB), 0, stream>>>(
+        rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
+        long_threshold, row_mask);
+  else if (live)
     k_spmm_layer<D, UNROLL, true><<<dim3((unsigned)blocks), dim3(64 * WPB), 0, stream>>>(
         rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, mode, denom,
         long_threshold, live);
@@ -253,13 +328,13 @@ static void launch_long(const int64_t *seg_beg, const int64_t *seg_end,
                         const int64_t *seg_ptr, int64_t n_long, const int32_t *src,
                         const float *dis, const float *w, const float *x, float *y,
                         const float *x0, float *acc, float *out, int mode, float denom,
-                        float *partial, hipStream_t stream) {
+                        float *partial, hipStream_t stream, const uint8_t *row_mask) {
   constexpr int UNROLL = (D <= 64) ? 4 : 8;
   if (n_seg > 0)
     k_spmm_segments<D, UNROLL><<<dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, stream>>>(
-        seg_beg, seg_end, seg_node, src, dis, w, x, partial, n_seg);
+        seg_beg, seg_end, seg_node, src, dis, w, x, partial, n_seg, row_mask);
   k_spmm_long_reduce<D><<<dim3((unsigned)((n_long + 3) / 4)), dim3(256), 0, stream>>>(
-      long_node, seg_ptr, partial, y, x0, acc, out, n_long, mode, denom);
+      long_node, seg_ptr, partial, y, x0, acc, out, n_long, mode, denom, row_mask);
 }
 
 static int check_modes(int acc_mode, const float *x0, const float *acc, const float *out,
@@ -285,7 +360,8 @@ static int spmm_layer(const int64_t *rowptr, const int32_t *src, const float *di
                       const float *w, const float *x, float *y, const float *x0, float *acc,
                       float *out, int64_t n_rows, int64_t row_offset, int32_t dim,
                       int32_t acc_mode, float denom, int64_t long_threshold,
-                      const uint8_t *live, lg_stream_t stream, const char *fn) {
+                      const uint8_t *live, lg_stream_t stream, const char *fn,
+                      const uint8_t *row_mask = nullptr) {
   LG_REQUIRE(rowptr && dis && x && n_rows >= 0 && row_offset >= 0,
              "%s: null pointer or negative size", fn);
   LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
@@ -296,10 +372,10 @@ static int spmm_layer(const int64_t *rowptr, const int32_t *src, const float *di
   if (long_threshold <= 0) long_threshold = INT64_MAX;
   hipStream_t s = (hipStream_t)stream;
   switch (dim) {
-    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
-    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
-    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
-    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s); break;
+    case 32: launch_spmm<32>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s, row_mask); break;
+    case 64: launch_spmm<64>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s, row_mask); break;
+    case 128: launch_spmm<128>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s, row_mask); break;
+    default: launch_spmm<256>(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, acc_mode, denom, long_threshold, live, s, row_mask); break;
   }
   return launch_status(fn);
 }
@@ -324,6 +400,31 @@ extern "C" int lg_spmm_layer_live_f32(const int64_t *rowptr, const int32_t *src,
                     acc_mode, denom, long_threshold, live, stream, "lg_spmm_layer_live_f32");
 }
 
+static int long_rows(const int64_t *seg_beg, const int64_t *seg_end, const int32_t *seg_node,
+                     int64_t n_seg, const int32_t *long_node, const int64_t *seg_ptr,
+                     int64_t n_long, const int32_t *src, const float *dis, const float *w,
+                     const float *x, float *y, const float *x0, float *acc, float *out,
+                     int32_t dim, int32_t acc_mode, float denom, float *partial,
+                     const uint8_t *row_mask, lg_stream_t stream, const char *fn) {
+  LG_REQUIRE(n_seg >= 0 && n_long >= 0, "%s: negative size", fn);
+  if (n_long == 0) return LG_OK;
+  LG_REQUIRE(seg_beg && seg_end && seg_node && long_node && seg_ptr && src && dis && x &&
+                 partial,
+             "%s: null pointer", fn);
+  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
+             "%s: dim %d not in {32,64,128,256}", fn, dim);
+  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, fn);
+  if (st != LG_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dim) {
+    case 32: launch_long<32>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s, row_mask); break;
+    case 64: launch_long<64>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s, row_mask); break;
+    case 128: launch_long<128>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s, row_mask); break;
+    default: launch_long<256>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s, row_mask); break;
+  }
+  return launch_status(fn);
+}
+
 extern "C" int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_end,
                                      const int32_t *seg_node, int64_t n_seg,
                                      const int32_t *long_node, const int64_t *seg_ptr,
@@ -332,21 +433,42 @@ extern "C" int lg_spmm_long_rows_f32(const int64_t *seg_beg, const int64_t *seg_
                                      const float *x0, float *acc, float *out, int32_t dim,
                                      int32_t acc_mode, float denom, float *partial,
                                      lg_stream_t stream) {
-  LG_REQUIRE(n_seg >= 0 && n_long >= 0, "lg_spmm_long_rows_f32: negative size");
-  if (n_long == 0) return LG_OK;
-  LG_REQUIRE(seg_beg && seg_end && seg_node && long_node && seg_ptr && src && dis && x &&
-                 partial,
-             "lg_spmm_long_rows_f32: null pointer");
-  LG_REQUIRE(dim == 32 || dim == 64 || dim == 128 || dim == 256,
-             "lg_spmm_long_rows_f32: dim %d not in {32,64,128,256}", dim);
-  const int st = check_modes(acc_mode, x0, acc, out, denom, x, y, "lg_spmm_long_rows_f32");
-  if (st != LG_OK) return st;
-  hipStream_t s = (hipStream_t)stream;
-  switch (dim) {
-    case 32: launch_long<32>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
-    case 64: launch_long<64>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
-    case 128: launch_long<128>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
-    default: launch_long<256>(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w, x, y, x0, acc, out, acc_mode, denom, partial, s); break;
-  }
-  return launch_status("lg_spmm_long_rows_f32");
+  return long_rows(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w,
+                   x, y, x0, acc, out, dim, acc_mode, denom, partial, nullptr, stream,
+                   "lg_spmm_long_rows_f32");
+}
+
+extern "C" int lg_spmm_long_rows_masked_f32(
+    const int64_t *seg_beg, const int64_t *seg_end, const int32_t *seg_node, int64_t n_seg,
+    const int32_t *long_node, const int64_t *seg_ptr, int64_t n_long, const int32_t *src,
+    const float *dis, const float *w, const float *x, float *y, const float *x0, float *acc,
+    float *out, int32_t dim, int32_t acc_mode, float denom, float *partial,
+    const uint8_t *row_mask, lg_stream_t stream) {
+  LG_REQUIRE(row_mask, "lg_spmm_long_rows_masked_f32: null row mask");
+  return long_rows(seg_beg, seg_end, seg_node, n_seg, long_node, seg_ptr, n_long, src, dis, w,
+                   x, y, x0, acc, out, dim, acc_mode, denom, partial, row_mask, stream,
+                   "lg_spmm_long_rows_masked_f32");
+}
+
+extern "C" int lg_spmm_layer_rows_f32(const int64_t *rowptr, const int32_t *src,
+                                      const float *dis, const float *w, const float *x,
+                                      float *y, const float *x0, float *acc, float *out,
+                                      int64_t n_rows, int64_t row_offset, int32_t dim,
+                                      int32_t acc_mode, float denom, int64_t long_threshold,
+                                      const uint8_t *row_mask, lg_stream_t stream) {
+  LG_REQUIRE(row_mask, "lg_spmm_layer_rows_f32: null row mask");
+  return spmm_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows, row_offset, dim,
+                    acc_mode, denom, long_threshold, nullptr, stream, "lg_spmm_layer_rows_f32",
+                    row_mask);
+}
+
+extern "C" int lg_mark_neighbors_u8(const int64_t *rowptr, const int32_t *src, int64_t n_rows,
+                                    const uint8_t *in_mask, uint8_t *out_mask,
+                                    lg_stream_t stream) {
+  LG_REQUIRE(rowptr && src && in_mask && out_mask && n_rows >= 0 && in_mask != out_mask,
+             "lg_mark_neighbors_u8: bad arguments");
+  if (n_rows == 0) return LG_OK;
+  k_mark_neighbors<<<dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream>>>(rowptr, src, n_rows, in_mask, out_mask);
+  return launch_status("lg_mark_neighbors_u8");
 }

@@ -464,7 +464,8 @@ constexpr int ring_chunk_bytes(int D, int W) {
   return 0;
 }
 
-template <int D, int NG, int WAVES, int M, int CAP, int NBUF, int LA, int LAG, bool SEEDP>
+template <int D, int NG, int WAVES, int M, int CAP, int NBUF, int LA, int LAG, bool SEEDP,
+          bool GL = false>
 __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const float *__restrict__ eu, const float *__restrict__ ei, const __bf16 *__restrict__ eub,
     const __bf16 *__restrict__ eib, const float *__restrict__ umarg, int64_t n_users,
@@ -472,12 +473,21 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     const int32_t *__restrict__ ex_col, float mask_value, int k, int n_splits,
     int64_t items_per_split, float *__restrict__ out_val, int64_t *__restrict__ out_idx,
     float *__restrict__ part_val, int32_t *__restrict__ part_idx,
-    const float *__restrict__ seed_val) {
+    const float *__restrict__ seed_val, uint2 *__restrict__ gl_list) {
   // WAVES waves x NG groups of 16 users (the MFMA columns); a list of CAP entries per user, up
   // to M per lane (entry e = 64 j + lane in slab j). The host picks CAP > k + 16 (k <= 32: 256
-  // users and CAP 56; k <= 64: 128 users and CAP 112; k <= 128: 128 users and CAP 160)
+  // users and CAP 56; k <= 64: 128 users and CAP 112; k <= 128: 128 users and CAP 160).
+  // GL (global lists): each user's list is a slab of CAPG = 64 M entries {key, item} in global
+  // memory (gl_list + (split n_users + user) CAPG, L2/MALL-resident), and the LDS holds only a
+  // staging list of CAP (<= 64) entries per user in front of it: insertions go to the staging
+  // list as above; one that could overflow on the next tile is spilled (appended to the slab:
+  // one store per entry), and a slab that could not take the next spill is compacted (the same
+  // compaction, on the slab). The LDS left over goes to the fragment ring, and the lists --
+  // which hold k + the entries inside the margins -- compact every CAPG - k - CAP insertions
+  // instead of every CAP - k - 16.
   static_assert(M == 1 || M == 2 || M == 4, "list slabs");
-  static_assert(CAP <= 64 * M && CAP > 32 * M, "list capacity");
+  static_assert(GL ? (CAP <= 64 && CAP > 16) : (CAP <= 64 * M && CAP > 32 * M), "list capacity");
+  constexpr int CAPG = 64 * M;  // (GL: the slab's capacity)
   constexpr int Q = D / 4;   // f32 MFMA steps
   constexpr int S = D / 32;  // bf16 MFMA k-blocks
   // the fragment ring: chunks of CI items (CB bytes, PPT 16-byte LDS-DMA pieces per thread)
@@ -520,6 +530,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   bool uvalid[NG];
   int64_t ex_pos[NG], ex_hi[NG];
   int cnt[NG], chk[NG];
+  int gcnt[NG];  // (GL) entries in the user's slab; chk: its count at the last compaction
   float thr[NG];
   float sthr[NG];  // the seeded floor of the threshold (-inf without a seed)
   // the entry threshold over a list's k-th lower bound tau and the seed floor st: an
@@ -559,8 +570,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     }
     cnt[g] = 0;
     chk[g] = 0;
+    gcnt[g] = 0;
     thr[g] = uvalid[g] ? entry_thr(neg_inf<float>(), sthr[g]) : __builtin_huge_valf();
   }
+  // (GL) the slab of user u of group g (valid users only: padding users never insert)
+  auto gslab = [&](int g, int u) __attribute__((always_inline)) {
+    return gl_list + ((int64_t)split * n_users + ubase + 16 * g + u) * CAPG;
+  };
 #ifdef LG_TOPK_COUNT
   // 0 inserted entries, 1 group-tiles with a hit, 2 compactions, 3 escapes (lists made exact
   // mid-stream), 4 exclusion-row loads, 5 entries ranked exactly at the end, 6 users finished;
@@ -584,7 +600,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     float uf[Q];
     user = user < n_users ? user : n_users - 1;  // (callers pass valid users; a clamp is cheap)
     load_piece<Q>(eu + user * D + gq * Q, uf);
-    constexpr int CS = CAP < 64 ? CAP : 64;            // entries of one slab
+    constexpr int CS = !GL && CAP < 64 ? CAP : 64;     // entries of one slab
     constexpr int NB = CS / 16 + (CS % 16 ? 1 : 0);    // 16-entry batches
     constexpr int BL = D <= 64 ? 4 : 2;               // batches whose rows load together
 #pragma unroll
@@ -634,15 +650,47 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   (NG == 1   ? (a)[0]                                                                           \
    : NG == 2 ? ((g) ? (a)[1 % NG] : (a)[0])                                                     \
              : ((g) == 0 ? (a)[0] : (g) == 1 ? (a)[1 % NG] : (g) == 2 ? (a)[2 % NG] : (a)[3 % NG]))
+  // (GL: the same on the user's slab, whose entries are {key, item}; the staging list is empty
+  // then -- compactions follow the user's spill -- and the slab's stores are waited first)
   auto compact_user = [&](int g, int u, int lim, bool fin, float (&ov)[M], int (&oi)[M])
       __attribute__((always_inline)) {
-    const int n = __shfl(gget(cnt, g), u);
+    const int n = __shfl(GL ? gget(gcnt, g) : gget(cnt, g), u);
     const int c0 = __shfl(gget(chk, g), u);
     int64_t pos = __shfl(gget(ex_pos, g), u);
     const int64_t hi = __shfl(gget(ex_hi, g), u);
     const float m = __shfl(gget(marg, g), u), st = __shfl(gget(sthr, g), u);
     uint32_t *ks = &lk[wave][g][u][0];
     uint16_t *ts = &lt[wave][g][u][0];
+    uint2 *slab = nullptr;
+    if constexpr (GL) {
+      slab = gslab(g, u);
+      // the spills' and the last compaction's stores have completed (in L2) before the slab is
+      // read, and the reads bypass the CU's L1 (agent-scope loads): the vector L1 may still
+      // hold the slab's lines from the last compaction's reads
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bool have[M], excl[M], keep[M];
+    float lb[M], hb[M];
+    uint32_t kbits[M];
+    int item[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int ej = 64 * j + lane;
+      have[j] = ej < n;
+      if constexpr (GL) {
+        const uint64_t e =
+            have[j] ? __hip_atomic_load(reinterpret_cast<uint64_t *>(slab + ej),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : 0ull;
+        kbits[j] = (uint32_t)e;
+        item[j] = (int)(uint32_t)(e >> 32);
+      } else {
+        kbits[j] = have[j] ? ks[ej] : 0u;
+        const int tix = have[j] ? (int)ts[ej] : 0;
+        item[j] = (int)i0 + (tix << 4) + (int)(kbits[j] & kRowMask);
+      }
+    }
+    // the lazy exclusion of the entries [c0, n), in registers
     if (n > c0) {
       while (pos < hi) {
         const int64_t e = pos + lane;
@@ -656,16 +704,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         for (int j = 0; j < M; ++j) {
           const int ej = 64 * j + lane;
           if (ej >= c0 && ej < n) {  // (entries since the last compaction: bound entries)
-            const uint32_t kbits = ks[ej];
-            const int item = (int)i0 + ((int)ts[ej] << 4) + (int)(kbits & kRowMask);
             int a = 0, b = nin;  // first index with exs[] >= item
             while (a < b) {
               const int mid = (a + b) >> 1;
-              if (exs[wave][mid] < item) a = mid + 1;
+              if (exs[wave][mid] < item[j]) a = mid + 1;
               else b = mid;
             }
-            if (a < nin && exs[wave][a] == item)
-              ks[ej] = key_pack(mask_value, (kbits & kRowMask) | kExact | kExcl);
+            if (a < nin && exs[wave][a] == item[j])
+              kbits[j] = key_pack(mask_value, (kbits[j] & kRowMask) | kExact | kExcl);
           }
         }
         wave_sync();
@@ -673,19 +719,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         if (nin < 64) break;
       }
     }
-    bool have[M], excl[M], keep[M];
-    float lb[M], hb[M];
-    uint32_t kbits[M];
-    uint16_t tix[M];
-    int item[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-      const int ej = 64 * j + lane;
-      have[j] = ej < n;
-      kbits[j] = have[j] ? ks[ej] : 0u;
-      tix[j] = have[j] ? ts[ej] : (uint16_t)0;
       excl[j] = (kbits[j] & kExcl) != 0;
-      item[j] = (int)i0 + ((int)tix[j] << 4) + (int)(kbits[j] & kRowMask);
       const float v = key_value(kbits[j]), mj = (kbits[j] & kExact) ? 0.f : m;
       lb[j] = excl[j] ? mask_value : lbound_t(v, mj);
       hb[j] = excl[j] ? mask_value : ubound_t(v, mj);
@@ -721,11 +757,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     // escape (make the list exact) when more entries stay than room for a tile; for the
     // 4-slab lists (k <= 128) already at k + 30: their exact k-th value then bounds the next
     // insertions (k = 100 at C5: 31.2 -> 28.2 ms; k + 18 / 24 / 36: 32.3 / 28.4 / 28.7 ms; the
-    // same for k <= 64 lists was slower). (Measurement builds: -DLG_RING_ESC=n escapes at > n.)
+    // same for k <= 64 lists was slower). GL: when the slab could not take the next spill.
+    // (Measurement builds: -DLG_RING_ESC=n escapes at > n.)
+    constexpr int ROOM = GL ? CAPG - CAP : CAP - 16;
 #ifdef LG_RING_ESC
-    const int esc = LG_RING_ESC < CAP - 16 ? LG_RING_ESC : CAP - 16;
+    const int esc = LG_RING_ESC < ROOM ? LG_RING_ESC : ROOM;
+#elif defined(LG_GL_ESC)  // (measurement builds: GL slabs escape at > k + LG_GL_ESC)
+    const int esc = !GL ? (M == 4 && k + 30 < ROOM ? k + 30 : ROOM)
+                        : (k + LG_GL_ESC < ROOM ? k + LG_GL_ESC : ROOM);
 #else
-    const int esc = M == 4 && k + 30 < CAP - 16 ? k + 30 : CAP - 16;
+    const int esc = !GL && M == 4 && k + 30 < ROOM ? k + 30 : ROOM;
 #endif
     LG_COUNT(3, (!fin && nk > esc) ? 1 : 0);
     LG_COUNT(5, fin ? nk : 0);
@@ -748,10 +789,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
       for (int j = 0; j < M; ++j) {
         const int ej = 64 * j + lane;
-        if (ej < nk) {  // (an exact score equal to the mask value may pass as excluded: the same)
+        if (ej < nk && !fin) {  // (an exact score equal to the mask value may pass as excluded: the same)
           const int rel = ii[j] - (int)i0;
-          ks[ej] = key_pack(kk[j], (uint32_t)(rel & 15) | kExact | (kk[j] == mask_value ? kExcl : 0u));
-          ts[ej] = (uint16_t)(rel >> 4);
+          const uint32_t key =
+              key_pack(kk[j], (uint32_t)(rel & 15) | kExact | (kk[j] == mask_value ? kExcl : 0u));
+          if constexpr (GL) {
+            slab[ej] = make_uint2(key, (uint32_t)ii[j]);
+          } else {
+            ks[ej] = key;
+            ts[ej] = (uint16_t)(rel >> 4);
+          }
         }
         if (nk == k && j == ((k - 1) >> 6)) tau = __shfl(kk[j], (k - 1) & 63);  // (uniform)
         ov[j] = ej < nk ? kk[j] : neg_inf<float>();
@@ -763,8 +810,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       for (int j = 0; j < M; ++j) {
         if (keep[j]) {
           const int p = base + __popcll(kb[j] & lanemask_lt());
-          ks[p] = kbits[j];
-          ts[p] = tix[j];
+          if constexpr (GL) {
+            slab[p] = make_uint2(kbits[j], (uint32_t)item[j]);
+          } else {
+            ks[p] = kbits[j];
+            ts[p] = (uint16_t)((item[j] - (int)i0) >> 4);
+          }
         }
         base += __popcll(kb[j]);
       }
@@ -774,7 +825,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
     for (int j = 0; j < NG; ++j)
       if (j == g && ul == u) {
-        cnt[j] = nk;
+        if constexpr (GL) gcnt[j] = nk;
+        else cnt[j] = nk;
         chk[j] = nk;
         ex_pos[j] = pos;
         thr[j] = uvalid[j] ? nthr : __builtin_huge_valf();
@@ -795,13 +847,47 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     int oi[M];
     compact_user(b >> 4, b & 15, lim, false, ov, oi);
   };
+  // (GL) append user u's staging list to its slab (lane e: entry e) and empty it
+  auto spill_user = [&](int g, int u) __attribute__((always_inline)) {
+    const int n = __shfl(gget(cnt, g), u);
+    const int gc = __shfl(gget(gcnt, g), u);
+    if (lane < n) {
+      const uint32_t kb = lk[wave][g][u][lane];
+      const int it = (int)i0 + ((int)lt[wave][g][u][lane] << 4) + (int)(kb & kRowMask);
+      gslab(g, u)[gc + lane] = make_uint2(kb, (uint32_t)it);
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+      if (j == g && ul == u) {
+        cnt[j] = 0;
+        gcnt[j] = gc + n;
+      }
+  };
   auto compact_over = [&](int lim) __attribute__((always_inline)) {
     uint64_t need = lists_over(CAP - 16);
     wave_sync();
-    while (need) {
-      const int b = __builtin_ctzll(need);
-      need &= need - 1;
-      compact_one(b, lim);
+    if constexpr (GL) {
+      uint64_t full = 0;  // slabs that could not take the next spill
+      while (need) {
+        const int b = __builtin_ctzll(need);
+        need &= need - 1;
+        spill_user(b >> 4, b & 15);
+      }
+      wave_sync();  // (the staging entries are read before the next insertions overwrite them)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        full |= (__ballot(gcnt[g] > CAPG - CAP) & 0xffffull) << (16 * g);
+      while (full) {
+        const int b = __builtin_ctzll(full);
+        full &= full - 1;
+        compact_one(b, lim);
+      }
+    } else {
+      while (need) {
+        const int b = __builtin_ctzll(need);
+        need &= need - 1;
+        compact_one(b, lim);
+      }
     }
   };
   // insertion of group g's bf16 products accb of tile t (lane (ul, gq): items 4 gq + r of the
@@ -812,7 +898,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       // (a NaN bound -- a NaN product or margin -- enters: its exact chain decides)
-      const bool cand = rel + r < n_valid && above(acc[r] + marg[g], thr[g]);
+      const bool cand = rel + r < n_valid && above(acc[r] + marg[g], thr[g]) &&
+                        (!GL || uvalid[g]);  // (GL: padding users have no slab)
       const uint64_t bal = __ballot(cand);
       LG_COUNT(0, __popcll(bal));
       if (bal) {
@@ -1148,6 +1235,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       if (user >= n_users) break;
       float v[M];
       int id[M];
+      if constexpr (GL) {  // the staging list's entries join the slab first
+        if (__shfl(gget(cnt, b >> 4), b & 15) > 0) spill_user(b >> 4, b & 15);
+      }
       compact_user(b >> 4, b & 15, lim_end, true, v, id);
 #pragma unroll
       for (int j = 0; j < M; ++j) {
@@ -1361,6 +1451,33 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
   out_val[u * k + k - 1] = m;
 }
 
+// Global-list (GL) shapes: 8 waves x 2 groups (256 users per block), staging lists of
+// LG_GL_CAP entries (48 KiB at 32), LG_GL_NBUF ring buffers issued LG_GL_LA chunks ahead. The
+// product uses them for k > 32 (slabs of 128 / 256 entries); k <= 32 keeps the LDS lists
+// unless built with -DLG_TOPK_GL32=1 (slabs of 128). -DLG_TOPK_LDS_LISTS=1 restores the LDS
+// lists for every k (measurement builds).
+#ifndef LG_GL_CAP
+#define LG_GL_CAP 32
+#endif
+#ifndef LG_GL_NBUF
+#define LG_GL_NBUF 13
+#endif
+#ifndef LG_GL_LA
+#define LG_GL_LA 7
+#endif
+#ifndef LG_TOPK_GL32
+#define LG_TOPK_GL32 0
+#endif
+#ifndef LG_TOPK_LDS_LISTS
+#define LG_TOPK_LDS_LISTS 0
+#endif
+// the list slabs (uint2 entries per user) of the screened kernel's main pass at this k
+static int screen_slab_m(int k) {
+  if (LG_TOPK_LDS_LISTS) return 0;
+  if (k <= 32) return LG_TOPK_GL32 ? 2 : 0;
+  return k <= 64 ? 2 : 4;
+}
+
 template <int D>
 static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float *ei,
                                  const __bf16 *eub, const __bf16 *eib, const float *umarg,
@@ -1368,40 +1485,59 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
                                  const int32_t *ex_col, float mask_value, int k, int n_splits,
                                  int64_t items_per_split, float *out_val, int64_t *out_idx,
                                  float *part_val, int32_t *part_idx, const float *seed_val,
-                                 hipStream_t stream) {
+                                 uint2 *gl_list, hipStream_t stream) {
   // one block per CU: the lists (6-byte entries) + the fragment ring. k <= 32: 256 users of
   // CAP 56 (84 KiB) + 9 ring buffers; k <= 64: 128 users (8 waves x 1 group) of CAP 112
-  // (84 KiB) + 9 buffers; k <= 128: 128 users of CAP 160 (120 KiB) + 4 buffers
-#define LG_RING_LAUNCH(NG, W, MM, CAP, NBUF, LA, LAG, SEEDP)                                  \
+  // (84 KiB) + 9 buffers; k <= 128: 128 users of CAP 160 (120 KiB) + 4 buffers. GL (the main
+  // pass at k > 32): 256 users of staging lists + LG_GL_NBUF buffers, lists in gl_list.
+#define LG_RING_LAUNCH(NG, W, MM, CAP, NBUF, LA, LAG, SEEDP, GLM)                             \
   {                                                                                           \
     const int64_t upb = (int64_t)(W) * (NG) * 16;                                             \
     const int64_t tiles = (n_users + upb - 1) / upb;                                          \
-    k_topk_ring<D, NG, W, MM, CAP, NBUF, LA, LAG, SEEDP>                                      \
+    k_topk_ring<D, NG, W, MM, CAP, NBUF, LA, LAG, SEEDP, GLM>                                 \
         <<<dim3((unsigned)(tiles * n_splits)), dim3(64 * (W)), 0, stream>>>(                  \
             eu, ei, eub, eib, umarg, n_users, n_items, ex_rowptr, ex_col, mask_value, k,      \
-            n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val);       \
+            n_splits, items_per_split, out_val, out_idx, part_val, part_idx, seed_val,        \
+            gl_list);                                                                         \
   }
-  if (M == 1 && seedp)
+  const int gm = seedp ? 0 : screen_slab_m(k);
+  if (gm == 2) {
+    LG_RING_LAUNCH(2, 8, 2, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
+  } else if (gm == 4) {
+    LG_RING_LAUNCH(2, 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
+  } else if (M == 1 && seedp) {
     LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
-                   LG_RING_LAG, true)
-  else if (M == 1)
+                   LG_RING_LAG, true, false)
+  } else if (M == 1) {
     LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
-                   LG_RING_LAG, false)
-  else if (M == 2 && seedp)
-    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, true)
-  else if (M == 2)
-    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, false)
-  else if constexpr (D > 64) {  // (the LG_RING4_* shapes apply to d <= 64)
-    if (seedp) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, true)
-    else LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, false)
+                   LG_RING_LAG, false, false)
+  } else if (M == 2 && seedp) {
+    LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, true, false)
+  } else if (M == 2) {
+    if (LG_TOPK_LDS_LISTS)
+      LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, false, false)
+  } else if constexpr (D > 64) {  // (the LG_RING4_* shapes apply to d <= 64)
+    if (seedp) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, true, false)
+    else if (LG_TOPK_LDS_LISTS) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, false, false)
   } else {
-    if (seedp) LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true)
-    else LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false)
+    if (seedp)
+      LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true, false)
+    else if (LG_TOPK_LDS_LISTS)
+      LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false, false)
   }
 #undef LG_RING_LAUNCH
 }
 
 static int cap_m(int k) { return k <= 32 ? 1 : (k <= 64 ? 2 : 4); }
+
+// the screened call's workspace: partial lists (several splits) and the GL list slabs
+static size_t screened_part_bytes(int64_t n_users, int k, int ns) {
+  return ns > 1 ? (size_t)ns * (size_t)n_users * (size_t)k * (sizeof(float) + sizeof(int32_t))
+                : 0;
+}
+static size_t screened_slab_bytes(int64_t n_users, int k, int ns) {
+  return (size_t)ns * (size_t)n_users * 64 * (size_t)screen_slab_m(k) * sizeof(uint2);
+}
 
 static int64_t split_len(int64_t n_items, int n_splits) {
   int64_t per = (n_items + n_splits - 1) / n_splits;
@@ -1427,6 +1563,17 @@ extern "C" size_t lg_score_topk_ws_bytes(int64_t n_users, int64_t n_items, int32
   if (n_items > 0 && n_splits >= 1) n_splits = screened_splits(n_items, n_splits);
   if (n_splits <= 1 || n_users <= 0 || k <= 0) return 0;
   return (size_t)n_splits * (size_t)n_users * (size_t)k * (sizeof(float) + sizeof(int32_t));
+}
+
+extern "C" size_t lg_score_topk_screened_ws_bytes(int64_t n_users, int64_t n_items,
+                                                  int32_t dim, int32_t k, int32_t n_splits) {
+  (void)dim;
+  if (n_users <= 0 || n_items <= 0 || n_items >= 0x7fffffff || k < 1 || k > 128 ||
+      n_splits < 1)
+    return 0;
+  const int64_t per = split_len(n_items, screened_splits(n_items, n_splits));
+  const int ns = (int)((n_items + per - 1) / per);
+  return screened_part_bytes(n_users, k, ns) + screened_slab_bytes(n_users, k, ns);
 }
 
 extern "C" int lg_score_topk_f32(const float *eu, const float *ei, int64_t n_users,
@@ -1502,23 +1649,28 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
   const int ns = (int)((n_items + per - 1) / per);
   float *part_val = nullptr;
   int32_t *part_idx = nullptr;
-  if (ns > 1) {
-    const size_t need = lg_score_topk_ws_bytes(n_users, n_items, dim, k, ns);
-    if (!ws || ws_bytes < need) {
+  uint2 *gl_list = nullptr;
+  {
+    const size_t part = screened_part_bytes(n_users, k, ns);
+    const size_t need = part + screened_slab_bytes(n_users, k, ns);
+    if (need > 0 && (!ws || ws_bytes < need)) {
       set_error("lg_score_topk_screened_f32: workspace %zu < %zu bytes", ws_bytes, need);
       return LG_ERR_WORKSPACE;
     }
-    part_val = (float *)ws;
-    part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+    if (ns > 1) {
+      part_val = (float *)ws;
+      part_idx = (int32_t *)((char *)ws + (size_t)ns * n_users * k * sizeof(float));
+    }
+    if (screen_slab_m(k)) gl_list = (uint2 *)((char *)ws + part);
   }
   hipStream_t s = (hipStream_t)stream;
   const int M = cap_m(k);
   const __bf16 *ub = (const __bf16 *)eu_bf16, *ib = (const __bf16 *)ei_bf16;
   auto pass = [&](bool seedp, int64_t n_it, int nsp, int64_t per_sp, const float *seed) {
     switch (dim) {
-      case 32: dispatch_topk_screen<32>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
-      case 64: dispatch_topk_screen<64>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
-      default: dispatch_topk_screen<128>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, s); break;
+      case 32: dispatch_topk_screen<32>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, gl_list, s); break;
+      case 64: dispatch_topk_screen<64>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, gl_list, s); break;
+      default: dispatch_topk_screen<128>(M, seedp, eu, ei, ub, ib, umarg, n_users, n_it, ex_rowptr, ex_col, mask_value, k, nsp, per_sp, out_val, out_idx, part_val, part_idx, seed, gl_list, s); break;
     }
     int st = launch_status("lg_score_topk_screened_f32");
     if (st != LG_OK || nsp == 1) return st;

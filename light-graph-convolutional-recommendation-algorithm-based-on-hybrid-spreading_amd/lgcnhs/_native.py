@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("LGCNHS_LIB_PATH") or LIB_PATH
 LG_OK = 0
 LG_ACC_NONE, LG_ACC_FIRST, LG_ACC_MID, LG_ACC_LAST, LG_ACC_ONLY = 0, 1, 2, 3, 4
 LG_EXCL_DROP, LG_EXCL_NONE = 0, 1
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -54,7 +54,19 @@ SIGNATURES = {
         [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
          _f32, _vp, _vp],
     ),
+    "lg_spmm_layer_rows_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _f32, _i64, _vp,
+         _vp],
+    ),
+    "lg_spmm_long_rows_masked_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+         _f32, _vp, _vp, _vp],
+    ),
+    "lg_mark_neighbors_u8": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "lg_score_topk_ws_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "lg_score_topk_screened_ws_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "lg_score_topk_f32": (
         ctypes.c_int,
         [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _f32, _i32, _i32, _vp, _vp, _vp, _sz, _vp],

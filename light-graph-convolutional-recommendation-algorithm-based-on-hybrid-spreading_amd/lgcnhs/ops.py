@@ -32,14 +32,23 @@ def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------ propagation
 def run_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows: int, row_offset: int,
-              mode: int, denom: float, plan=None, live=None) -> None:
+              mode: int, denom: float, plan=None, live=None, row_mask=None) -> None:
     """One propagation layer over a CSR slice: lg_spmm_layer_f32 for the ordinary rows (or
-    lg_spmm_layer_live_f32 when a uint8 per-node ``live`` mask marks x's non-zero rows)
-    and, when the slice has rows above the long-row threshold, lg_spmm_long_rows_f32."""
+    lg_spmm_layer_live_f32 when a uint8 per-node ``live`` mask marks x's non-zero rows, or
+    lg_spmm_layer_rows_f32 computing only the rows a uint8 per-node ``row_mask`` marks)
+    and, when the slice has rows above the long-row threshold, lg_spmm_long_rows_f32 (its
+    masked form with row_mask)."""
     dim = x.shape[1]
     thr = plan.threshold if (plan is not None and plan.n_long) else 0
     strm = N.stream_handle(x.device)
-    if live is not None:
+    if row_mask is not None:
+        if live is not None:
+            raise ValueError("row_mask and live are exclusive")
+        N.check(N.lib().lg_spmm_layer_rows_f32(
+            N.ptr(rowptr), N.ptr(src), N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0),
+            N.ptr(acc), N.ptr(out), n_rows, row_offset, dim, mode, float(denom), thr,
+            N.ptr(row_mask), strm), "lg_spmm_layer_rows_f32")
+    elif live is not None:
         if live.dtype != torch.uint8 or live.numel() != x.shape[0] or live.device != x.device:
             raise ValueError("live must be a uint8 mask with one entry per row of x")
         N.check(N.lib().lg_spmm_layer_live_f32(
@@ -53,21 +62,26 @@ def run_layer(rowptr, src, dis, w, x, y, x0, acc, out, n_rows: int, row_offset: 
             "lg_spmm_layer_f32")
     if thr:
         part = plan.partial(dim, x.device)
-        N.check(N.lib().lg_spmm_long_rows_f32(
-            N.ptr(plan.seg_beg), N.ptr(plan.seg_end), N.ptr(plan.seg_node), plan.n_seg,
-            N.ptr(plan.long_node), N.ptr(plan.seg_ptr), plan.n_long, N.ptr(src), N.ptr(dis),
-            N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out), dim, mode,
-            float(denom), N.ptr(part), strm), "lg_spmm_long_rows_f32")
+        args = (N.ptr(plan.seg_beg), N.ptr(plan.seg_end), N.ptr(plan.seg_node), plan.n_seg,
+                N.ptr(plan.long_node), N.ptr(plan.seg_ptr), plan.n_long, N.ptr(src),
+                N.ptr(dis), N.ptr(w), N.ptr(x), N.ptr(y), N.ptr(x0), N.ptr(acc), N.ptr(out),
+                dim, mode, float(denom), N.ptr(part))
+        if row_mask is not None:
+            N.check(N.lib().lg_spmm_long_rows_masked_f32(*args, N.ptr(row_mask), strm),
+                    "lg_spmm_long_rows_masked_f32")
+        else:
+            N.check(N.lib().lg_spmm_long_rows_f32(*args, strm), "lg_spmm_long_rows_f32")
 
 
 def spmm_layer(adj: Adjacency, x: torch.Tensor, y, x0, acc, out, mode: int, denom: float,
-               stream_weights: bool = True, long_rows: bool = True, live=None) -> None:
-    """One layer over all rows of ``adj``; with stream_weights the precomputed gcn_norm
-    edge weights are streamed (else recomputed from dis; identical values); with
-    long_rows, hub rows go through the segmented path."""
+               stream_weights: bool = True, long_rows: bool = True, live=None,
+               row_mask=None) -> None:
+    """One layer over all rows of ``adj`` (or the rows ``row_mask`` marks); with
+    stream_weights the precomputed gcn_norm edge weights are streamed (else recomputed from
+    dis; identical values); with long_rows, hub rows go through the segmented path."""
     w = adj.edge_weight() if stream_weights else None
     run_layer(adj.rowptr, adj.src, adj.dis(), w, x, y, x0, acc, out, adj.n_nodes, 0, mode,
-              denom, adj.long_plan() if long_rows else None, live)
+              denom, adj.long_plan() if long_rows else None, live, row_mask)
 
 
 LIVE_FRACTION = 0.25  # below this share of non-zero input rows, skip the dead rows' gathers
@@ -115,6 +129,99 @@ def propagate_mean(adj: Adjacency, e0: torch.Tensor, layers: int,
         spmm_layer(adj, x, y, e0, out, out, mode, layers + 1, live=live)
         x = y
     return out
+
+
+RESTRICT_FRACTION = 0.5  # a layer whose needed rows may exceed this share runs in full
+
+
+def row_masks(adj: Adjacency, nodes: torch.Tensor, layers: int, force: bool = False) -> list:
+    """Per layer l (0-based) the uint8 mask of the rows whose layer-l output the final
+    embeddings at ``nodes`` depend on, or None for a full layer: layer L-1 at the nodes, each
+    layer below also at the sources of the rows above it (lg_mark_neighbors_u8). A layer
+    runs in full once its rows may exceed RESTRICT_FRACTION of the graph (estimated without a
+    host sync: |nodes| times (1 + mean degree) per layer down), and so does every layer below
+    it. ``force`` masks every layer (tests)."""
+    n = adj.n_nodes
+    masks = [None] * layers
+    if layers == 0:
+        return masks
+    est = min(n, int(nodes.numel()))
+    m = torch.zeros(n, dtype=torch.uint8, device=nodes.device)
+    m[nodes] = 1
+    strm = N.stream_handle(nodes.device)
+    for l in range(layers - 1, -1, -1):
+        if not force and est > RESTRICT_FRACTION * n:
+            break
+        masks[l] = m
+        if l > 0:
+            m2 = torch.zeros_like(m)
+            N.check(N.lib().lg_mark_neighbors_u8(N.ptr(adj.rowptr), N.ptr(adj.src), n,
+                                                 N.ptr(m), N.ptr(m2), strm),
+                    "lg_mark_neighbors_u8")
+            m = m2
+            est = min(n, est * (1 + -(-adj.nnz // max(1, n))))
+    return masks
+
+
+def propagate_rows_mean(adj: Adjacency, e0: torch.Tensor, layers: int, nodes: torch.Tensor,
+                        force_masks: bool = False) -> torch.Tensor:
+    """propagate_mean's output at the rows ``nodes`` (int64, duplicates allowed), each row
+    bitwise the full forward's: layer l computes only the rows row_masks marks (the training
+    step's forward: the BPR loss reads the final embeddings at the mini-batch's <= 3 x batch
+    rows only, reference model/LightGCN/train.py:30-45)."""
+    e0 = _f32(e0, "e0")
+    if e0.shape[0] != adj.n_nodes:
+        raise ValueError(f"e0 has {e0.shape[0]} rows, graph has {adj.n_nodes} nodes")
+    nodes = nodes.to(device=e0.device, dtype=torch.int64)
+    if layers <= 0:
+        return e0[nodes]
+    masks = row_masks(adj, nodes, layers, force_masks)
+    out = torch.empty_like(e0)
+    bufs = [torch.empty_like(e0), torch.empty_like(e0) if layers > 2 else None]
+    x = e0
+    for l in range(layers):
+        first, last = l == 0, l == layers - 1
+        if first and last:
+            mode = N.LG_ACC_ONLY
+        elif first:
+            mode = N.LG_ACC_FIRST
+        elif last:
+            mode = N.LG_ACC_LAST
+        else:
+            mode = N.LG_ACC_MID
+        y = None if last else bufs[l % 2]
+        spmm_layer(adj, x, y, e0, out, out, mode, layers + 1, row_mask=masks[l])
+        x = y
+    return out[nodes]
+
+
+class _PropagateRows(torch.autograd.Function):
+    """Forward: the final embeddings at ``nodes`` (output-restricted layers). Backward: the
+    full operator's, grad_e0 = mean_l (A_hat^T)^l g with g scattered to the nodes' rows --
+    what the full forward followed by the gather gives."""
+
+    @staticmethod
+    def forward(ctx, e0, adj, layers, nodes):
+        ctx.adj, ctx.layers, ctx.n = adj, layers, e0.shape[0]
+        ctx.save_for_backward(nodes)
+        return propagate_rows_mean(adj, e0.detach(), layers, nodes)
+
+    @staticmethod
+    def backward(ctx, g):
+        (nodes,) = ctx.saved_tensors
+        gfull = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
+        gfull.index_add_(0, nodes, g)
+        gin = propagate_mean(ctx.adj.transpose(), gfull, ctx.layers, sparse_input=True)
+        return gin, None, None, None
+
+
+def propagate_rows(adj: Adjacency, e0: torch.Tensor, layers: int,
+                   nodes: torch.Tensor) -> torch.Tensor:
+    """propagate(adj, e0, layers)[nodes], computing only the rows it needs."""
+    nodes = nodes.to(device=e0.device, dtype=torch.int64)
+    if e0.requires_grad and torch.is_grad_enabled():
+        return _PropagateRows.apply(e0, adj, layers, nodes)
+    return propagate_rows_mean(adj, e0, layers, nodes)
 
 
 class PropagationGraph:
@@ -177,8 +284,8 @@ def _resident_blocks(device, k: int = 64, screen: bool = False) -> int:
 
 def _users_per_block(k: int, screen: bool = False) -> int:
     """Users per workgroup of csrc/topk.hip's launches (dispatch_topk / _screen)."""
-    if screen:
-        return 256 if k <= 32 else 128
+    if screen:  # (k > 32: the global-list shape, 8 waves x 2 groups)
+        return 256
     return 128 if k <= 32 else (64 if k <= 64 else 32)
 
 
@@ -254,7 +361,9 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
         raise ValueError(f"exclusion rows {excl.n_rows} != users {nu}")
     ns = (_splits_for(nu, ni, k, _resident_blocks(eu.device, k, screen), screen)
           if n_splits is None else int(n_splits))
-    ws_bytes = N.lib().lg_score_topk_ws_bytes(nu, ni, d, k, ns)
+    ws_fn = (N.lib().lg_score_topk_screened_ws_bytes if screen and nu > 0
+             else N.lib().lg_score_topk_ws_bytes)
+    ws_bytes = ws_fn(nu, ni, d, k, ns)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
     val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)
     idx = torch.empty((nu, k), dtype=torch.int64, device=eu.device)

@@ -36,6 +36,14 @@ class LightGCN(nn.Module):
         users_final, items_final = torch.split(emb_final, [self.user_num, self.item_num])
         return users_final, w_u, items_final, w_i
 
+    def forward_rows(self, edge_index, nodes: torch.Tensor) -> torch.Tensor:
+        """The final embeddings of forward() at node ids ``nodes`` (users 0..U-1, items
+        U..U+I-1), computing each layer only at the rows those depend on (the training step,
+        whose loss reads the mini-batch's rows only); each row bitwise forward()'s."""
+        w_u, w_i = self.users_emb.weight, self.items_emb.weight
+        adj = as_adjacency(edge_index, self.user_num + self.item_num, device=w_u.device)
+        return ops.propagate_rows(adj, torch.cat([w_u, w_i]), self.layers, nodes)
+
     def message(self, x_j, norm) -> torch.Tensor:
         """PyG message hook of the reference (:76-84); the fused kernel applies it inline."""
         return norm.view(-1, 1) * x_j

@@ -26,12 +26,24 @@ from utils.wrapper import calTimes
 
 def getEmbeddingForBPR(model, user_num: int, item_num: int, train_edge_index,
                        batch_size: int, device, r_edge_index=None) -> tuple:
-    """Reference :26-59."""
-    users_final, users_0, items_final, items_0 = model.forward(train_edge_index)
+    """Reference :26-59: the mini-batch's final and initial embeddings. The reference runs
+    the full forward and then gathers the batch's rows; here the batch is drawn first (the
+    forward draws no random numbers, so the triples are the same) and a model with
+    ``forward_rows`` computes each layer only where those rows depend on it (layer L at the
+    <= 3 x batch rows, layer L-1 there and at their neighbours, ...), bitwise the same rows."""
     if r_edge_index is None:
         r_edge_index = convertAdjMatrixToEdgeIndex(user_num, item_num, train_edge_index)
     u, p, n = sampleMiniBatch(batch_size, r_edge_index.to(device), item_num)
-    return (users_final[u], users_0[u], items_final[p], items_0[p], items_final[n], items_0[n])
+    rows = getattr(model, "forward_rows", None)
+    if rows is None:
+        users_final, users_0, items_final, items_0 = model.forward(train_edge_index)
+        return (users_final[u], users_0[u], items_final[p], items_0[p], items_final[n],
+                items_0[n])
+    u, p, n = u.long(), p.long(), n.long()
+    f = rows(train_edge_index, torch.cat([u, user_num + p, user_num + n]))
+    fu, fp, fn = torch.split(f, [u.numel(), p.numel(), n.numel()])
+    users_0, items_0 = model.users_emb.weight, model.items_emb.weight
+    return (fu, users_0[u], fp, items_0[p], fn, items_0[n])
 
 
 class ValidationState:

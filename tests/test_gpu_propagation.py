@@ -263,3 +263,46 @@ def test_live_mask_backward_equals_dense(dist, dim):
     with pytest.raises(ValueError):
         ops.spmm_layer(adj, g, y2, None, None, None, N.LG_ACC_NONE, 1.0,
                        live=live.to(torch.int32))
+
+
+@pytest.mark.parametrize("dist,force", [("uniform", False), ("uniform", True), ("zipf", False),
+                                        ("zipf", True)])
+@pytest.mark.parametrize("L", [1, 2, 3, 4])
+def test_restricted_forward_rows_equal_full_forward(dist, force, L):
+    """The training step's forward (ops.propagate_rows: each layer only at the rows the
+    mini-batch's final embeddings depend on, lg_spmm_layer_rows_f32 / the masked segmented
+    path for hub rows / lg_mark_neighbors_u8) gives the full forward's rows bit for bit, with
+    duplicate nodes, under the default layer plan (full below the restricted layers) and with
+    every layer masked; its gradient equals the full forward + gather's."""
+    from lgcnhs import ops
+    from lgcnhs.graph import Adjacency
+    U, I, E = (60_000, 5_000, 600_000) if dist == "zipf" else (40_000, 30_000, 300_000)
+    users, items = _synth_graph(U, I, E, seed=7, dist=dist)
+    adj = Adjacency.from_interactions(torch.as_tensor(users), torch.as_tensor(items), U, I, DEV)
+    if dist == "zipf":
+        assert adj.long_plan().n_long > 0
+    n, d = U + I, 64
+    gen = torch.Generator(device=DEV).manual_seed(L)
+    e0 = torch.randn(n, d, device=DEV, generator=gen) * 0.1
+    nodes = torch.cat([torch.randint(0, U, (300,), device=DEV, generator=gen),
+                       U + torch.randint(0, I, (600,), device=DEV, generator=gen)])
+    nodes[5] = nodes[17]  # a duplicate
+    if dist == "zipf":  # the hub items' rows (segmented path) among the nodes
+        deg = adj.rowptr[1:] - adj.rowptr[:-1]
+        nodes[:8] = torch.topk(deg, 8).indices
+    full = ops.propagate(adj, e0, L)
+    got = ops.propagate_rows_mean(adj, e0, L, nodes, force_masks=force)
+    assert torch.equal(got, full[nodes])
+    masks = ops.row_masks(adj, nodes.long(), L, force=force)
+    assert masks[L - 1] is not None and int(masks[L - 1].sum()) == int(torch.unique(nodes).numel())
+    if force or L == 1:
+        assert all(m is not None for m in masks)
+    # autograd: the restricted rows' gradient = the full forward's + the gather's (distinct
+    # nodes: no accumulation order in between)
+    nd = torch.unique(nodes)
+    w = torch.randn(nd.numel(), d, device=DEV, generator=gen)
+    a = e0.clone().requires_grad_(True)
+    (ops.propagate_rows(adj, a, L, nd) * w).sum().backward()
+    b = e0.clone().requires_grad_(True)
+    (ops.propagate(adj, b, L)[nd] * w).sum().backward()
+    assert torch.equal(a.grad, b.grad)

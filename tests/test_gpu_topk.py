@@ -104,7 +104,7 @@ def _screened_direct(eu, ei, k, ex, umarg, n_splits=1):
     ni = ei.shape[0]
     ub, _ = ops.bound_operands(eu)
     ib, _ = ops.bound_operands(ei)
-    ws_bytes = N.lib().lg_score_topk_ws_bytes(nu, ni, d, k, n_splits)
+    ws_bytes = N.lib().lg_score_topk_screened_ws_bytes(nu, ni, d, k, n_splits)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=eu.device)
     val = torch.empty((nu, k), dtype=torch.float32, device=eu.device)
     idx = torch.empty((nu, k), dtype=torch.int64, device=eu.device)
@@ -288,15 +288,18 @@ def test_bound_prep_rounds_and_bounds(d, n):
         assert ((got - ref) <= 1e-6 * ref + 1e-38).all()
 
 
-def test_screened_topk_catalog_over_2_20_items():
+@pytest.mark.parametrize("k", [20, 100])
+def test_screened_topk_catalog_over_2_20_items(k):
     """The screened kernel's list entries hold a 16-bit tile index, so lg_score_topk_screened_f32
     splits a catalog of more than 2^20 items (here 1,100,017: two splits even when one is asked
     for, the workspace sized by lg_score_topk_ws_bytes for it): bit-exact vs the C oracle, with
     a 20-user block whose best items sit past item 2^20."""
     from lgcnhs import _native as N
     from lgcnhs import ops
-    U, I, k = 96, 1_100_017, 20
+    U, I = 96, 1_100_017
     assert N.lib().lg_score_topk_ws_bytes(U, I, 64, k, 1) == 2 * U * k * 8
+    assert N.lib().lg_score_topk_screened_ws_bytes(U, I, 64, k, 1) == \
+        2 * U * k * 8 + (0 if k <= 32 else 2 * U * 256 * 8)
     eu, ei = _emb(U, 64, 61), _emb(I, 64, 62)
     ei[(1 << 20) + 5:(1 << 20) + 25] = eu[:20] * 3.0  # user u's best item: 2^20 + 5 + u
     rp, col = _excl(U, I, 2e-5, 63)

@@ -95,6 +95,11 @@ def test_argument_validation_without_gpu():
     # catalogs of more than 2^20 items: the screened kernel's splits (16-bit tile indices)
     assert lib.lg_score_topk_ws_bytes(100, (1 << 20) + 1, 64, 10, 1) == 2 * 100 * 10 * 8
     assert lib.lg_score_topk_ws_bytes(100, 1 << 20, 64, 10, 1) == 0
+    # the screened call: k <= 32 keeps its lists in LDS; above, one slab per user and split
+    assert lib.lg_score_topk_screened_ws_bytes(100, 1000, 64, 10, 1) == 0
+    assert lib.lg_score_topk_screened_ws_bytes(100, 1000, 64, 64, 1) == 100 * 128 * 8
+    assert lib.lg_score_topk_screened_ws_bytes(100, 1000, 64, 100, 3) == \
+        3 * 100 * 100 * 8 + 3 * 100 * 256 * 8
 
 
 def test_missing_library_fails_loudly(tmp_path):
