@@ -690,9 +690,23 @@ __global__ __launch_bounds__(256) void k_group_rows(
   }
 }
 
+__device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
+  __hip_atomic_fetch_add(&acc[col], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Hub rows of the group (flat index t * n_items + i of rows with bound > vthr, listed by
-// k_hub_list over the [n_tiles][n_items] bounds): k_tile_rows_hub's block-wide dense LDS
-// accumulation, on tile t's cursor cur[v] + (v's items in tiles < t).
+// k_hub_list over the [n_tiles][n_items] bounds): the dense accumulation of k_tile_rows_hub --
+// general_W[i][j] = the sum over i's users v, ascending, of fl(1/k_v) for each of v's items j
+// in tile t (on tile t's cursor cur[v] + v's items in tiles < t) -- by ONE WAVE per row, on
+// its own LDS accumulator. A hub item has up to all the users; the per-user metadata (the
+// user id, its 32-byte count record, its cursor and fl(1/k_v)) of 64 users is loaded by the
+// wave's lanes at once, and their items (~1-3 per user and tile) up to 256 at a time, each
+// lane finding the user of its entries by a binary search over the users' running counts;
+// the adds then go out user by user in ascending order, each an LDS atomic over the lanes
+// holding that user's entries. A wave's LDS operations are performed in order, so every
+// column is summed in ascending user order -- k_tile_rows_hub's sums, bit for bit -- with no
+// block barrier per user (that kernel's 256-thread block waited at one per user, and walked
+// the users one dependent load chain at a time).
 __global__ __launch_bounds__(256) void k_group_rows_hub(
     const int64_t *__restrict__ hub_rows, const int64_t *__restrict__ n_hub,
     const int64_t *__restrict__ item_rowptr, const int32_t *__restrict__ item_users,
@@ -701,66 +715,121 @@ __global__ __launch_bounds__(256) void k_group_rows_hub(
     int32_t group_begin, int32_t tile, int32_t stop, const int64_t *__restrict__ bound,
     int64_t vthr, const int64_t *__restrict__ units_incl, uint32_t *__restrict__ lines,
     uint32_t *__restrict__ ovf, int32_t *__restrict__ row_len) {
-  extern __shared__ double acc[];  // tile doubles
-  __shared__ int wsum[4];
+  extern __shared__ double lds_acc[];  // tile doubles per wave
+  const int nwb = blockDim.x / 64, wave = threadIdx.x / 64, lane = lane_id();
+  double *acc = lds_acc + (size_t)wave * tile;
   const int64_t nh = *n_hub;
-  for (int64_t h = blockIdx.x; h < nh; h += gridDim.x) {
+  for (int64_t h = (int64_t)blockIdx.x * nwb + wave; h < nh; h += (int64_t)gridDim.x * nwb) {
     const int64_t flat = hub_rows[h];
     const int t = (int)(flat / n_items);
     const int64_t i = flat - (int64_t)t * n_items;
     const int32_t item_begin = group_begin + t * tile;
-    for (int j = threadIdx.x; j < tile; j += blockDim.x) acc[j] = 0.0;
-    __syncthreads();
-    for (int64_t e = item_rowptr[i]; e < item_rowptr[i + 1]; ++e) {
-      const int32_t v = item_users[e];
-      const uint4 lo = counts[2 * (int64_t)v], hi = counts[2 * (int64_t)v + 1];
-      const int c = (int)count_of2(lo, hi, t);
-      if (c == 0) continue;  // uniform across the block: no barrier skipped unevenly
-      int64_t s0 = cur[v];
-      for (int q = 0; q < t; ++q) s0 += count_of2(lo, hi, q);
-      const double wv = inv_deg[v];
-      for (int q = threadIdx.x; q < c; q += blockDim.x) acc[user_items[s0 + q] - item_begin] += wv;
-      __syncthreads();  // the next user may hit the same columns from other threads
+    for (int j = lane; j < tile; j += 64) acc[j] = 0.0;
+    wave_sync();
+    const int64_t eb = item_rowptr[i], ee = item_rowptr[i + 1];
+    for (int64_t e0 = eb; e0 < ee; e0 += 64) {
+      const int64_t e = e0 + lane;
+      int c = 0;
+      int64_t s0 = 0;
+      double wv = 0.0;
+      if (e < ee) {
+        const int32_t v = item_users[e];
+        const uint4 lo = counts[2 * (int64_t)v], hi = counts[2 * (int64_t)v + 1];
+        c = (int)count_of2(lo, hi, t);
+        s0 = cur[v];
+        for (int q = 0; q < t; ++q) s0 += count_of2(lo, hi, q);
+        wv = inv_deg[v];
+      }
+      int incl = c;  // inclusive running count of the users' items (lane order = user order)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const int total = __shfl(incl, 63);
+      const int pos = incl - c;
+      uint64_t users = __ballot(c > 0);
+      if (total <= 256) {
+        // entry p = r * 64 + lane: the (p - pos_l)-th item of the user l with
+        // pos_l <= p < incl_l (the first lane whose running count passes p)
+        int col[4];
+        double wt[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 64 * r + lane;
+          col[r] = 0;
+          wt[r] = 0.0;
+          if (64 * r >= total) continue;  // (uniform)
+          int lo = 0, hi = 63;
+#pragma unroll
+          for (int st = 0; st < 6; ++st) {  // first lane l with incl_l > p
+            const int mid = (lo + hi) >> 1;
+            if (__shfl(incl, mid) > p) hi = mid;
+            else lo = mid + 1;
+          }
+          const int64_t s0l = __shfl(s0, lo);
+          const int pl = __shfl(pos, lo);
+          const double wl = __shfl(wv, lo);
+          if (p < total) {
+            col[r] = user_items[s0l + (p - pl)] - item_begin;
+            wt[r] = wl;
+          }
+        }
+        while (users) {
+          const int l = __builtin_ctzll(users);
+          users &= users - 1;
+          const int pl = __builtin_amdgcn_readlane(pos, l);
+          const int ql = __builtin_amdgcn_readlane(incl, l);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (64 * r >= ql || 64 * r + 64 <= pl) continue;  // (uniform)
+            const int p = 64 * r + lane;
+            if (p >= pl && p < ql) lds_add(acc, (uint32_t)col[r], wt[r]);
+          }
+        }
+      } else {  // (a chunk of users with more than 256 items in the tile: user by user)
+        while (users) {
+          const int l = __builtin_ctzll(users);
+          users &= users - 1;
+          const int cl = __builtin_amdgcn_readlane(c, l);
+          const int64_t s0l = __shfl(s0, l);
+          const double wl = __shfl(wv, l);
+          for (int q = lane; q < cl; q += 64)
+            lds_add(acc, (uint32_t)(user_items[s0l + q] - item_begin), wl);
+        }
+      }
     }
+    wave_sync();
     uint32_t *line = lines + (int64_t)t * (n_items + 1) * 32 + i * 32;
     const int64_t tbase = t ? units_incl[(int64_t)t * n_items - 1] : 0;
     uint32_t *ov = ovf + tbase * 4;
     const int64_t ou = units_incl[flat] -
                        run_units(bound[flat], vthr, tile_width(group_begin, tile, t, stop)) - tbase;
     int base = 0;
-    for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
-      const int j = j0 + threadIdx.x;
-      const bool nz = j < tile && acc[j] != 0.0;
+    for (int j0 = 0; j0 < tile; j0 += 64) {
+      const int j = j0 + lane;
+      const double x = j < tile ? acc[j] : 0.0;
+      const bool nz = x != 0.0;
       const uint64_t b = __ballot(nz);
-      const int w = threadIdx.x / 64;
-      if (lane_id() == 0) wsum[w] = __popcll(b);
-      __syncthreads();
-      int before_w = 0, total = 0;
-      for (int q = 0; q < 4; ++q) {
-        if (q < w) before_w += wsum[q];
-        total += wsum[q];
-      }
       if (nz) {
-        const uint64_t bits = (uint64_t)__double_as_longlong(acc[j]);
-        const int64_t e = base + before_w + __popcll(b & lanemask_lt());
-        uint32_t *u4 = e < kLineEnts ? line + 4 * (1 + e) : ov + 4 * (ou + 1 + (e - kLineEnts));
+        const uint64_t bits = (uint64_t)__double_as_longlong(x);
+        const int64_t en = base + __popcll(b & lanemask_lt());
+        uint32_t *u4 = en < kLineEnts ? line + 4 * (1 + en) : ov + 4 * (ou + 1 + (en - kLineEnts));
         *reinterpret_cast<uint4 *>(u4) =
             uint4{kEntV | (uint32_t)j, (uint32_t)bits, (uint32_t)(bits >> 32), 0u};
       }
-      base += total;
-      __syncthreads();
+      base += __popcll(b);
     }
     const bool has_ovf = base > kLineEnts;
-    if (threadIdx.x < 32) {
-      const int tw = threadIdx.x;  // line word
+    if (lane < 32) {
+      const int tw = lane;  // line word
       const int unit = tw / 4;
       if (tw == 0) line[0] = kHdrV | kHdrSlow | (has_ovf ? (kHdrOvf | (uint32_t)ou) : 0u);
       else if (unit == 0 || unit > base) line[tw] = 0u;
     }
-    if (has_ovf && threadIdx.x < 4)
-      ov[ou * 4 + threadIdx.x] = threadIdx.x == 0 ? (uint32_t)(base - kLineEnts) : 0u;
-    if (threadIdx.x == 0 && row_len) row_len[flat] = base;
-    __syncthreads();
+    if (has_ovf && lane < 4) ov[ou * 4 + lane] = lane == 0 ? (uint32_t)(base - kLineEnts) : 0u;
+    if (lane == 0 && row_len) row_len[flat] = base;
+    wave_sync();
   }
 }
 
@@ -1167,9 +1236,6 @@ __host__ __device__ constexpr size_t walk_shared_bytes(int tile) {
   return (size_t)kInvTab * 8 + 16 * 8 + (size_t)((tile + 1) & ~1) * 8 + 64 * 8;
 }
 
-__device__ __forceinline__ void lds_add(double *acc, uint32_t col, double v) {
-  __hip_atomic_fetch_add(&acc[col], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // The fast decode's two LDS addresses of a P slot s (class << 16 | column, column < 8192),
 // one VALU op each: fl(1/k) of the class at byte s >> 13 (s_inv at LDS address 0; bits
@@ -1220,6 +1286,12 @@ __device__ __forceinline__ void add_unit(double *acc, uint4 w, bool head, double
   if (py) lds_add(acc, py & 0xFFFFu, v1);
   if (pz) lds_add(acc, pz & 0xFFFFu, v2);
   if (pw) lds_add(acc, pw & 0xFFFFu, v3);
+}
+
+// A unit of a V row's overflow run: one entry (or a zero padding unit), ra * general_W into
+// its column (add_unit's V case without its four class reads of P slots)
+__device__ __forceinline__ void add_unit_v(double *acc, uint4 w, double ra) {
+  if (w.x & kEntV) lds_add(acc, w.x & 0xFFFFu, __hiloint2double((int)w.z, (int)w.y) * ra);
 }
 
 // Fast decode (P rows whose classes are all < kInvTab): s_inv sits at LDS address 0.
@@ -1483,7 +1555,7 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         const uint64_t bal = __ballot(o);
         if (o) {
           const int p = nov + __popcll(bal & lanemask_lt());
-          ovl_ent[p] = w[q].x & kHdrPtr;
+          ovl_ent[p] = w[q].x & (kHdrPtr | kHdrV);  // (the run's first unit; a V row's bit)
           ovl_ra[p] = ra[q];
         }
         nov += __popcll(bal);
@@ -1493,10 +1565,13 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         uint4 y4[4];
         uint32_t ou4[4];
         double r4[4];
+        bool v4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bool in = t0 + j < nov;
-          ou4[j] = ovl_ent[in ? t0 + j : t0];
+          const uint32_t e = ovl_ent[in ? t0 + j : t0];
+          v4[j] = (e & kHdrV) != 0;
+          ou4[j] = e & kHdrPtr;
           r4[j] = ovl_ra[in ? t0 + j : t0];
           y4[j] = a.ovf[(int64_t)ou4[j] + lane];
         }
@@ -1505,11 +1580,23 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           if (t0 + j >= nov) continue;
           const uint32_t n = (uint32_t)__shfl((int)y4[j].x, 0);
           if (lane == 0 || (uint32_t)lane > n) y4[j] = uint4{0u, 0u, 0u, 0u};
-          add_unit(acc, y4[j], false, r4[j], s_inv, a.g_inv);
-          for (uint32_t c = 64; c <= n; c += 64) {  // runs longer than 63 units
-            const uint32_t cc = c + lane;
-            const uint4 y = cc <= n ? a.ovf[(int64_t)ou4[j] + cc] : uint4{0u, 0u, 0u, 0u};
-            add_unit(acc, y, false, r4[j], s_inv, a.g_inv);
+          if (v4[j]) add_unit_v(acc, y4[j], r4[j]);
+          else add_unit(acc, y4[j], false, r4[j], s_inv, a.g_inv);
+          // runs longer than 63 units (hub items' V rows: up to a whole tile of entries): 4
+          // chunks of 64 units in flight per round instead of one load -> add at a time
+          for (uint32_t c = 64; c <= n; c += 256) {
+            uint4 z[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              const uint32_t cc = c + 64 * p + lane;
+              z[p] = cc <= n ? a.ovf[(int64_t)ou4[j] + cc] : uint4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              if (c + 64 * p > n) break;  // (uniform)
+              if (v4[j]) add_unit_v(acc, z[p], r4[j]);
+              else add_unit(acc, z[p], false, r4[j], s_inv, a.g_inv);
+            }
           }
         }
       }
@@ -2154,7 +2241,9 @@ extern "C" int lg_spread_group_rows_f64(
   const int64_t nflat = n_items * n_tiles;
   k_hub_list<<<dim3((unsigned)((nflat + 255) / 256)), dim3(256), 0, s>>>(
       bound, nflat, vthr, (unsigned long long *)n_hub, hub_rows);
-  k_group_rows_hub<<<dim3(1024), dim3(256), (size_t)tile * sizeof(double), s>>>(
+  const int hub_waves = tile <= 4096 ? 4 : 2;  // (LDS: one tile of doubles per wave)
+  k_group_rows_hub<<<dim3(1024), dim3(64 * hub_waves), (size_t)hub_waves * tile * sizeof(double),
+                     s>>>(
       hub_rows, n_hub, item_rowptr, item_users, user_items, inv_deg, n_items, cur, c4,
       group_begin, tile, stop, bound, vthr, units_incl, (uint32_t *)lines, (uint32_t *)ovf,
       row_len);

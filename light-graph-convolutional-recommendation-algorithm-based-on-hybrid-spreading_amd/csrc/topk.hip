@@ -874,9 +874,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         spill_user(b >> 4, b & 15);
       }
       wave_sync();  // (the staging entries are read before the next insertions overwrite them)
+#ifdef LG_GL_TRIG  // (measurement builds: compact once a slab holds more than k + LG_GL_TRIG)
+      const int trig = k + LG_GL_TRIG < CAPG - CAP ? k + LG_GL_TRIG : CAPG - CAP;
+#else
+      const int trig = CAPG - CAP;
+#endif
 #pragma unroll
       for (int g = 0; g < NG; ++g)
-        full |= (__ballot(gcnt[g] > CAPG - CAP) & 0xffffull) << (16 * g);
+        full |= (__ballot(gcnt[g] > trig) & 0xffffull) << (16 * g);
       while (full) {
         const int b = __builtin_ctzll(full);
         full &= full - 1;
@@ -1399,6 +1404,9 @@ static bool lg_topk_seeding() { return LG_TOPK_SEED != 0; }
 #ifndef LG_TOPK_SEED_DIV  // the seed pass covers the first 1/LG_TOPK_SEED_DIV of the items
 #define LG_TOPK_SEED_DIV 16
 #endif
+#ifndef LG_TOPK_SEED_DIV_HI  // ... for k > 32
+#define LG_TOPK_SEED_DIV_HI 16
+#endif
 
 template <int D, int NG, int M, int WAVES>
 static void launch_topk(const float *eu, const float *ei, int64_t n_users, int64_t n_items,
@@ -1468,6 +1476,9 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
 #ifndef LG_TOPK_GL32
 #define LG_TOPK_GL32 0
 #endif
+#ifndef LG_GL_NG  // user groups per wave in the GL shapes (4: 512 users per block)
+#define LG_GL_NG 2
+#endif
 #ifndef LG_TOPK_LDS_LISTS
 #define LG_TOPK_LDS_LISTS 0
 #endif
@@ -1502,9 +1513,9 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
   }
   const int gm = seedp ? 0 : screen_slab_m(k);
   if (gm == 2) {
-    LG_RING_LAUNCH(2, 8, 2, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
+    LG_RING_LAUNCH(LG_GL_NG, 8, 2, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
   } else if (gm == 4) {
-    LG_RING_LAUNCH(2, 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
+    LG_RING_LAUNCH(LG_GL_NG, 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
   } else if (M == 1 && seedp) {
     LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
                    LG_RING_LAG, true, false)
@@ -1693,7 +1704,7 @@ extern "C" int lg_score_topk_screened_f32(const float *eu, const float *ei, cons
   // pass reads it there before it writes anything: a user's seed and its list belong to the
   // same wave), on at most as many splits as the main pass (their seeds fit the same
   // workspace; the largest is kept)
-  const int64_t n_seed = n_items / LG_TOPK_SEED_DIV / 16 * 16;
+  const int64_t n_seed = n_items / (k > 32 ? LG_TOPK_SEED_DIV_HI : LG_TOPK_SEED_DIV) / 16 * 16;
   const bool seeded = lg_topk_seeding() && n_seed >= (int64_t)k * 64;
   if (seeded) {
     const int64_t per_s = split_len(n_seed, ns);

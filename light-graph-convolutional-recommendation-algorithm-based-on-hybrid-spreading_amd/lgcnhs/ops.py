@@ -812,6 +812,7 @@ class TileWeights:
             hub = self.is_hub
             ln = self.row_len[:I].to(torch.int64)
             self.paths_read += (self.row_uses * ln).sum()
+            self.paths_hub += (self.row_uses * ln * hub[:I]).sum()  # (V rows' share)
             used = _run_units(ln, hub)
             self.bytes_read += 128 * self.row_uses.sum() + 16 * (self.row_uses * used).sum()
 
@@ -891,6 +892,7 @@ def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,
         stats["nch"] = -(-tile // 64) if walk.d else 0
     if stats is not None and count_paths:
         stats["w_paths"] = stats.get("w_paths", 0) + int(tw.paths_read)
+        stats["w_paths_hub"] = stats.get("w_paths_hub", 0) + int(tw.paths_hub)
         stats["w_bytes"] = stats.get("w_bytes", 0) + int(tw.bytes_read)
     return vals, idxs
 
@@ -901,6 +903,7 @@ def _count_rows(tw: "TileWeights", A: Interactions, u0: int, u1: int) -> None:
     cols = A.by_user.col[int(A.by_user.rowptr[u0]):int(A.by_user.rowptr[u1])]
     tw.row_uses = torch.bincount(cols, minlength=A.n_items).to(torch.int64)
     tw.paths_read = torch.zeros((), dtype=torch.int64, device=A.k_item.device)
+    tw.paths_hub = torch.zeros((), dtype=torch.int64, device=A.k_item.device)
     tw.bytes_read = torch.zeros((), dtype=torch.int64, device=A.k_item.device)
 
 

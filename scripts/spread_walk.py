@@ -38,7 +38,7 @@ if a.identity_classes:
     ops.degree_classes = _identity_classes
 dev = torch.device("cuda:0")
 U, I, E, D, _ = bench.WORKLOADS[a.workload]
-_, _, keys = bench.gen_graph(U, I, E, 0, dev)
+_, _, keys = bench.gen_graph(U, I, E, 0, dev, dist=bench.GRAPH_DIST.get(a.workload, "uniform"))
 A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, dev)
 del keys
 g = torch.Generator(device=dev).manual_seed(42)
@@ -55,7 +55,8 @@ for rep in range(a.reps):
     torch.cuda.synchronize()
     dt = time.time() - t
     print(f"rep {rep}: {a.tiles} tiles x {U} users: {dt:.3f} s"
-          + (f"  paths {st.get('w_paths', 0):.3e} bytes {st.get('w_bytes', 0):.3e}"
+          + (f"  paths {st.get('w_paths', 0):.3e} (V rows {st.get('w_paths_hub', 0):.3e})"
+             f" bytes {st.get('w_bytes', 0):.3e}"
              f"  build {st.get('t_build_ms', 0):.1f} ms bounds {st.get('t_bounds_ms', 0):.1f} ms"
              f" walk {st.get('t_walk_ms', 0):.1f} ms" if st else ""), flush=True)
     h = (idxs.to(torch.float64) * torch.arange(1, 21, device=dev, dtype=torch.float64)).sum()
