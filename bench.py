@@ -325,7 +325,7 @@ def time_exchange(prop, shard, D, world, dev, reps=5):
             "recv_bytes_per_gpu": recv, "pad_ratio": shard.pad_ratio}
 
 
-def bench_other_graph(name, dev, steps, k, topk_users, cpu_parity=True):
+def bench_other_graph(name, dev, steps, k, topk_users, cpu_parity=True, spread=False):
     """A second graph shape at N = 1 (SURVEY.md §8(d)'s power-law input): the propagation
     (K1 with the long-row pass for hub rows inside the timed forward) with its roofline and
     PMC traffic, the degree profile that drives it, and the masked top-K on the same graph's
@@ -383,6 +383,13 @@ def bench_other_graph(name, dev, steps, k, topk_users, cpu_parity=True):
         out["topk"] = topk
     except Exception as ex:  # a side measurement never hides the main result
         log(f"{name} topk bench failed: {ex!r}")
+    if spread:  # LGCNHS on this graph (all users), its walk roofline, the V-row share, parity
+        try:
+            torch.cuda.empty_cache()
+            out["spread"] = bench_spread(keys, U, I, e0, k, 0, 1, dev, extras=False,
+                                         parity=cpu_parity)
+        except Exception as ex:  # a side measurement never hides the main result
+            log(f"{name} spread bench failed: {ex!r}")
     del e0, keys
     torch.cuda.empty_cache()
     return out
@@ -576,7 +583,8 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, e
     dt = time.perf_counter() - t0
     # the walk's paths / row bytes: counted from the tiles after the timed run (untimed)
     i0, i1 = item_range(I, tile, rank, world)
-    st["w_paths"], st["w_bytes"] = ops.tile_traffic(A, tile, items=slice(i0, i1))
+    st["w_paths"], st["w_bytes"], st["w_paths_v"] = ops.tile_traffic(A, tile,
+                                                                   items=slice(i0, i1), hub=True)
     paths, nbytes = float(st["w_paths"]), float(st["w_bytes"])
     if world > 1:
         e = torch.tensor([paths, nbytes], dtype=torch.float64, device=dev)
@@ -620,6 +628,9 @@ def bench_spread(keys, U, I, e0_orig, k, rank, world, dev, lam=0.5, tile=2048, e
     res = {"recs_per_s": U / dt, "users": U, "dim": int(eu.shape[1]), "seconds": dt, "k": k,
            "lambda": lam, "paths_per_s": paths / dt, "row_bytes_GBps": nbytes / dt / 1e9,
            "tile": tile, "filled_frac_rank0": filled, "roofline": walk,
+           # the paths' split between P rows (one 4-byte slot per (user, item) pair) and V
+           # rows (hub items: merged general_W entries, one 16-byte unit per column)
+           "paths_v_rows_share": (st["w_paths_v"] / st["w_paths"]) if st["w_paths"] else None,
            "sharding": f"item range x{world} + all-to-all of per-range top-k lists",
            "path": "lg_spread_group_{cursor,bound,rows} + lg_score_chunk_bound (bf16 MFMA) + "
                    "lg_spread_tile_resource_topk_f64 (fused walk) + lg_topk_lists_merge_f64"}
@@ -948,7 +959,9 @@ def main():
     ap.add_argument("--layout", default="bipartite", choices=["bipartite", "rows"],
                     help="N>1 row sharding: users and items sharded separately with "
                          "cross-layer overlap (bipartite) or contiguous node rows (rows)")
-    ap.add_argument("--other-graphs", nargs="*", default=["c5-zipf-d64"],
+    ap.add_argument("--spread-graphs", nargs="*", default=["c4-zipf"],
+                    help="N = 1: of --other-graphs, also run LGCNHS (all users) on these")
+    ap.add_argument("--other-graphs", nargs="*", default=["c5-zipf-d64", "c4-zipf"],
                     help="N = 1: also measure these graph shapes (other_graphs; the Zipf(1.1) "
                          "power-law input of SURVEY.md §8(d))")
     ap.add_argument("--launch-check", action="store_true",
@@ -1076,7 +1089,8 @@ def main():
             try:
                 other_graphs[name.split("-d")[0].replace("c5-", "").replace("c4-", "c4_")] = \
                     bench_other_graph(name, dev, max(3, args.steps // 2), args.k,
-                                      args.topk_users, cpu_parity=not args.no_cpu_baseline)
+                                      args.topk_users, cpu_parity=not args.no_cpu_baseline,
+                                      spread=name in args.spread_graphs)
             except Exception as ex:  # a side measurement never hides the main result
                 log(f"{name} bench failed: {ex!r}")
             torch.cuda.empty_cache()

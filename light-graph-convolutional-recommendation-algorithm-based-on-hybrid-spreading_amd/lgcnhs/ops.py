@@ -908,20 +908,23 @@ def _count_rows(tw: "TileWeights", A: Interactions, u0: int, u1: int) -> None:
 
 
 def tile_traffic(A: Interactions, tile: int = 2048, users: slice | None = None,
-                 items: slice | None = None) -> tuple[int, int]:
+                 items: slice | None = None, hub: bool = False) -> tuple:
     """(paths, row bytes) the tile walk of users / items gathers (the stats of
-    spread_topk_tiled(count_paths=True)), from the tiles alone: builds every tile, no walk."""
+    spread_topk_tiled(count_paths=True)), from the tiles alone: builds every tile, no walk;
+    with ``hub`` also the paths that come from V (hub) rows: (paths, row bytes, V paths)."""
     u0, u1 = (0, A.n_users) if users is None else (users.start, users.stop)
     i0, i1 = (0, A.n_items) if items is None else (max(0, items.start),
                                                    min(A.n_items, items.stop))
     if i1 <= i0 or u1 <= u0:
-        return 0, 0
+        return (0, 0, 0) if hub else (0, 0)
     tw = TileWeights(A, 0.5, min(int(tile), i1 - i0))
     if i0:
         tw.seek(i0)
     _count_rows(tw, A, u0, u1)
     for j0 in range(i0, i1, tw.tile):
         tw.build(j0, stop=i1)
+    if hub:
+        return int(tw.paths_read), int(tw.bytes_read), int(tw.paths_hub)
     return int(tw.paths_read), int(tw.bytes_read)
 
 

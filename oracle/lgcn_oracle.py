@@ -355,8 +355,34 @@ def spread_row_paths(urp, uit, irp, ius, n_items: int, u: int, lam: float,
     return np.bincount(j_p, weights=w_p, minlength=n_items) / beta
 
 
+def spread_rows_spmv(urp, uit, irp, ius, n_items: int, users, lam: float) -> np.ndarray:
+    """The rows ``users`` of F = A @ HybridS(A, getSpreadingGeneralMat(A), lam)
+    (model/SpreadMethod/model.py:14-27, :63-85, :88-99) as two sparse products instead of
+    the path enumeration of spread_row_paths: with X = A[users] / k_i^(1-lam) (one row per
+    user), C = X A^T (the users' co-occurrence with every user v, weighted by 1/k_i^(1-lam)),
+    F = (C / k_v) A / k_j^lam -- the same sum regrouped (v before j), fp64; for hub-heavy
+    (Zipf) graphs, where a user's 3-hop paths run into the 10^9 (every hub item's users'
+    items), it costs two SpMMs over the interactions per block. k == 0 -> 1 as the reference."""
+    import scipy.sparse as sp
+    urp, uit = np.asarray(urp, np.int64), np.asarray(uit, np.int64)
+    irp = np.asarray(irp, np.int64)
+    n_users = urp.size - 1
+    k_u = np.diff(urp).astype(np.float64)
+    k_u[k_u == 0] = 1
+    k_i = np.diff(irp).astype(np.float64)
+    alpha, beta = np.power(k_i, 1 - lam), np.power(k_i, lam)
+    alpha[alpha == 0] = 1
+    beta[beta == 0] = 1
+    A = sp.csr_matrix((np.ones(uit.size), uit, urp), shape=(n_users, n_items))
+    X = sp.diags(np.ones(len(users))) @ A[np.asarray(users, np.int64)] @ sp.diags(1.0 / alpha)
+    C = (X @ A.T).toarray()                      # [len(users), n_users]
+    C /= k_u[None, :]
+    return np.asarray((A.T @ C.T).T) / beta[None, :]
+
+
 def spread_parity(got_idx, users, urp, uit, irp, ius, n_items: int, lam: float, eu, ei,
-                  k: int, dim_tol: int | None = None, block: int = 64):
+                  k: int, dim_tol: int | None = None, block: int = 64,
+                  method: str = "auto"):
     """LGCNHS (SpreadLightGCN, model/SpreadLightGCN/model.py:122-153 + recommend.py:18-52)
     top-k lists ``got_idx`` [len(users), k] of ``users`` against this oracle: S = G * F with
     F = spread_row_paths and G the e0 score (eu[u] . ei[j], judged in exact fp64), every
@@ -365,7 +391,9 @@ def spread_parity(got_idx, users, urp, uit, irp, ius, n_items: int, lam: float, 
     item that could rank in the top k). A user is *identical* if the sets agree,
     *tie-affected* if every differing item's exact S lies within the two methods' rounding
     bounds (G: 2 gamma_d sum|u_k i_k| for the fp32 dot of either side; F: 1e-12 relative) of
-    the reference's k-th exact S, else *mismatched*. Returns the counts."""
+    the reference's k-th exact S, else *mismatched*. Returns the counts. F comes from
+    spread_row_paths, or (method "spmv", or "auto" when a block's users have more than
+    2 x 10^8 three-hop paths: hub-heavy graphs) from spread_rows_spmv."""
     urp, uit = np.asarray(urp, np.int64), np.asarray(uit, np.int64)
     irp, ius = np.asarray(irp, np.int64), np.asarray(ius, np.int64)
     eu, ei = np.asarray(eu, np.float32), np.asarray(ei, np.float32)
@@ -383,12 +411,20 @@ def spread_parity(got_idx, users, urp, uit, irp, ius, n_items: int, lam: float, 
     users = np.asarray(users, np.int64)
     out = {"users": int(users.size), "k": k, "identical": 0, "tie_affected": 0,
            "mismatched": 0, "first_mismatch": None}
+    # three-hop paths behind each user: sum over its items i of sum over i's users v of k_v
+    p_item = np.add.reduceat(k_u[ius], irp[:-1]) if ius.size else np.zeros(n_items)
+    p_item[np.diff(irp) == 0] = 0
     for b0 in range(0, users.size, block):
         ub = users[b0:b0 + block]
         G32 = eu[ub] @ ei.T                      # fp32 screen of G for the block
         Gb = np.abs(eu[ub]) @ ei_abs.T           # sum |u_k i_k| (fp32, rounded up below)
+        paths = sum(float(p_item[uit[urp[u]:urp[u + 1]]].sum()) for u in ub.tolist())
+        Fb = None
+        if method == "spmv" or (method == "auto" and paths > 2e8):
+            Fb = spread_rows_spmv(urp, uit, irp, ius, n_items, ub, lam)
         for r, u in enumerate(ub.tolist()):
-            F = spread_row_paths(urp, uit, irp, ius, n_items, u, lam, inv_ku, alpha, beta)
+            F = Fb[r] if Fb is not None else \
+                spread_row_paths(urp, uit, irp, ius, n_items, u, lam, inv_ku, alpha, beta)
             own = uit[urp[u]:urp[u + 1]]
             gtol = gam * Gb[r].astype(np.float64) * (1 + 1e-6) + 1e-30
             s32 = G32[r].astype(np.float64) * F

@@ -244,6 +244,37 @@ def test_c4_zipf_forward_every_row():
     np.testing.assert_allclose(out, acc / 4, rtol=0, atol=TOL)
 
 
+def test_c4_zipf_lgcnhs_sampled_users_vs_oracle():
+    """SpreadLightGCN on the power-law graph (c4-zipf: 200K x 200K, 20M Zipf(1.1)
+    interactions; the top items are held by most users, so their W rows are dense V rows in
+    every tile and carry most of the 3-hop paths) for ALL users through the tiled walk, then
+    256 users -- the 16 highest-degree, the first and the last, random ones -- against the
+    oracle (its regrouped sparse-product F, spread_rows_spmv, where a user's paths run into
+    the 10^9) times the exact e0 dot product, every interaction dropped: 0 mismatched,
+    tie-affected <= 1 %."""
+    from lgcnhs import ops
+    from lgcnhs.synth import synth_graph_device
+    U = I = 200_000
+    lam, k = 0.5, 20
+    _, _, keys = synth_graph_device(U, I, 20_000_000, seed=6, device=DEV, dist="zipf")
+    A = ops.Interactions.from_pairs(keys // I, keys % I, U, I, DEV)
+    g = torch.Generator(DEV).manual_seed(43)
+    eu = torch.randn(U, 64, device=DEV, generator=g) * 0.1
+    ei = torch.randn(I, 64, device=DEV, generator=g) * 0.1
+    _, got = ops.spread_topk_tiled(A, lam, k, A.by_user, True, eu, ei)
+    users = _lgcnhs_sample(A, U, n=256, top=16)
+    got = got[torch.as_tensor(users, device=DEV)].cpu().numpy()
+    deg_i = A.k_item.cpu().numpy()
+    assert deg_i.max() > 0.5 * U  # hub items held by most users
+    r = O.spread_parity(got, users, A.by_user.rowptr.cpu().numpy(), A.by_user.col.cpu().numpy(),
+                        A.by_item.rowptr.cpu().numpy(), A.by_item.col.cpu().numpy(), I, lam,
+                        eu.cpu().numpy(), ei.cpu().numpy(), k)
+    print(f"[c4-zipf LGCNHS top-20] {len(users)} users: identical {r['identical']}, "
+          f"tie-affected {r['tie_affected']}, mismatched {r['mismatched']}")
+    assert r["mismatched"] == 0, r["first_mismatch"]
+    assert r["tie_affected"] <= max(1, len(users) // 100)
+
+
 @pytest.fixture(scope="module")
 def c5zipf():
     from lgcnhs.synth import synth_graph_device

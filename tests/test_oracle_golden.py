@@ -175,9 +175,33 @@ def test_spread_row_paths_equals_reference_F(golden, name):
                                    atol=1e-15 * np.abs(g[f"F_{j}"]).max())
 
 
-def test_spread_parity_counts_reference_lists(golden):
+@pytest.mark.parametrize("name", ["spread_toy", "spread_edge", "spread_ml100k"])
+def test_spread_rows_spmv_equals_reference_F(golden, name):
+    """The regrouped restatement for hub-heavy graphs (spread_rows_spmv: two sparse products,
+    the checker of the Zipf LGCNHS parity) against the reference's own F matrices where the
+    fixture holds them, and against the path-order rows (spread_row_paths) everywhere."""
+    g = golden(name)
+    U, I, A = _spread_case(g)
+    uu, ii = np.nonzero(A)
+    urp = np.searchsorted(uu, np.arange(U + 1))
+    order = np.lexsort((uu, ii))
+    irp = np.searchsorted(ii[order], np.arange(I + 1))
+    users = np.arange(U) if U <= 64 else np.array([0, 1, 5, 17, 100, U - 1])
+    lams = [float(x) for x in g["lambdas"]] if "lambdas" in g else [0.0, 0.5, 1.0]
+    for j, lam in enumerate(lams):
+        Fm = O.spread_rows_spmv(urp, ii, irp, uu[order], I, users, lam)
+        Fp = np.stack([O.spread_row_paths(urp, ii, irp, uu[order], I, u, lam) for u in users])
+        np.testing.assert_allclose(Fm, Fp, rtol=1e-13, atol=1e-16 * max(1.0, np.abs(Fp).max()))
+        if f"F_{j}" in g:
+            ref = g[f"F_{j}"][users]
+            np.testing.assert_allclose(Fm, ref, rtol=1e-12, atol=1e-15 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("method", ["paths", "spmv"])
+def test_spread_parity_counts_reference_lists(golden, method):
     """spread_parity on lists taken from the dense restatement (G * F, interactions
-    dropped): every user identical; a corrupted list is counted as mismatched."""
+    dropped): every user identical; a corrupted list is counted as mismatched -- with F from
+    the path enumeration and from the regrouped sparse products."""
     g = golden("spread_ml100k")
     U, I, A = _spread_case(g)
     F = O.get_resource(A, O.hybrid_s(A, O.spreading_general_mat(A.copy()), 0.5))
@@ -192,9 +216,10 @@ def test_spread_parity_counts_reference_lists(golden):
     order = np.lexsort((uu, ii))
     irp = np.searchsorted(ii[order], np.arange(I + 1))
     users = np.arange(0, U, 7)
-    r = O.spread_parity(ref[users], users, urp, ii, irp, uu[order], I, 0.5, eu, ei, 10)
+    r = O.spread_parity(ref[users], users, urp, ii, irp, uu[order], I, 0.5, eu, ei, 10,
+                        method=method)
     assert r["identical"] == users.size and r["mismatched"] == 0
     bad = ref[users].copy()
     bad[0, 3] = int(np.argsort(S[users[0]])[I // 2])  # a mid-ranked item
     assert O.spread_parity(bad, users, urp, ii, irp, uu[order], I, 0.5, eu, ei,
-                           10)["mismatched"] == 1
+                           10, method=method)["mismatched"] == 1
