@@ -72,6 +72,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //   entry per distinct column, ascending: {0x80000000 | (j - item_begin), fp64
 //   general_W[i][j] (lo, hi), 0}; line units 1..7 hold the first 7, the overflow units one
 //   each.
+//   A V row with more than width / 2 + 8 entries (hub items held by a large share of the
+//   users: nearly every column) is DENSE instead: its line holds only the header, and its
+//   overflow run (header x = kRunDense | n, n = ceil(width / 2) data units) holds the row's
+//   general_W of columns 2q and 2q + 1 in unit q as two fp64 (zeros included) -- 8 bytes per
+//   column instead of 16 per entry, read with no column index (the walk's hub rows are bound
+//   by these reads). The sparse run's allocation (1 + min(pairs, width) - 7 units) covers it.
 // Neither format depends on lambda (ra / rb are applied by the walk), so a lambda sweep
 // reuses the built tiles.
 constexpr uint32_t kHdrV = 0x80000000u;
@@ -79,6 +85,7 @@ constexpr uint32_t kHdrOvf = 0x40000000u;
 constexpr uint32_t kHdrSlow = 0x20000000u;
 constexpr uint32_t kHdrPtr = 0x1FFFFFFFu;
 constexpr uint32_t kEntV = 0x80000000u;
+constexpr uint32_t kRunDense = 0x80000000u;  // overflow run header: a dense V row
 constexpr int kLineSlots = 31;  // P slots in a line (word 0 is the header)
 constexpr int kLineEnts = 7;    // V entries in a line (unit 0 holds the header)
 constexpr int kInvTab = 512;    // degree classes whose fl(1/k) is cached in LDS
@@ -158,6 +165,22 @@ __device__ __forceinline__ void put_slot(uint32_t *__restrict__ line, uint32_t *
                                          int64_t ou, int64_t p, uint32_t w) {
   if (p < kLineSlots) line[1 + p] = w;
   else ovf[(ou + 1) * 4 + (p - kLineSlots)] = w;
+}
+
+// The dense form of a V row from its accumulator acc[0 .. width) (threads t = t0 .. of a
+// stride-ts group write): the line's header and zero words, the run header, the data units.
+__device__ __forceinline__ bool hub_row_dense(int nz, int width) { return nz > width / 2 + 8; }
+__device__ void write_hub_row_dense(const double *acc, int width, uint32_t *line, uint32_t *ov,
+                                    int64_t ou, int t0, int ts) {
+  const int nd = (width + 1) / 2;
+  for (int t = t0; t < 32; t += ts) line[t] = t == 0 ? (kHdrV | kHdrSlow | kHdrOvf | (uint32_t)ou) : 0u;
+  for (int t = t0; t < 4; t += ts) ov[ou * 4 + t] = t == 0 ? (kRunDense | (uint32_t)nd) : 0u;
+  for (int q = t0; q < nd; q += ts) {
+    const uint64_t a = (uint64_t)__double_as_longlong(acc[2 * q]);
+    const uint64_t b = 2 * q + 1 < width ? (uint64_t)__double_as_longlong(acc[2 * q + 1]) : 0ull;
+    *reinterpret_cast<uint4 *>(ov + 4 * (ou + 1 + q)) =
+        uint4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+  }
 }
 
 #if LG_REFERENCE_PATHS
@@ -248,6 +271,22 @@ __global__ __launch_bounds__(256) void k_tile_rows_hub(
     }
     uint32_t *line = lines + i * 32;
     const int64_t ou = ovf_ptr[i];
+    if (threadIdx.x == 0) wsum[0] = 0;
+    __syncthreads();
+    {
+      int c = 0;
+      for (int j = threadIdx.x; j < tile; j += blockDim.x) c += acc[j] != 0.0;
+      atomicAdd(&wsum[0], c);
+    }
+    __syncthreads();
+    const int nzr = wsum[0];
+    __syncthreads();
+    if (hub_row_dense(nzr, tile)) {  // (tile = this tile's width here)
+      write_hub_row_dense(acc, tile, line, ovf, ou, threadIdx.x, blockDim.x);
+      if (threadIdx.x == 0 && row_len) row_len[i] = nzr;
+      __syncthreads();
+      continue;
+    }
     int base = 0;
     for (int j0 = 0; j0 < tile; j0 += blockDim.x) {
       const int j = j0 + threadIdx.x;
@@ -803,8 +842,17 @@ __global__ __launch_bounds__(256) void k_group_rows_hub(
     uint32_t *line = lines + (int64_t)t * (n_items + 1) * 32 + i * 32;
     const int64_t tbase = t ? units_incl[(int64_t)t * n_items - 1] : 0;
     uint32_t *ov = ovf + tbase * 4;
-    const int64_t ou = units_incl[flat] -
-                       run_units(bound[flat], vthr, tile_width(group_begin, tile, t, stop)) - tbase;
+    const int width = (int)tile_width(group_begin, tile, t, stop);
+    const int64_t ou = units_incl[flat] - run_units(bound[flat], vthr, width) - tbase;
+    int nzr = 0;
+    for (int j0 = 0; j0 < tile; j0 += 64)
+      nzr += __popcll(__ballot(j0 + lane < tile && acc[j0 + lane] != 0.0));
+    if (hub_row_dense(nzr, width)) {
+      write_hub_row_dense(acc, width, line, ov, ou, lane, 64);
+      if (lane == 0 && row_len) row_len[flat] = nzr;
+      wave_sync();
+      continue;
+    }
     int base = 0;
     for (int j0 = 0; j0 < tile; j0 += 64) {
       const int j = j0 + lane;
@@ -1293,6 +1341,12 @@ __device__ __forceinline__ void add_unit(double *acc, uint4 w, bool head, double
 __device__ __forceinline__ void add_unit_v(double *acc, uint4 w, double ra) {
   if (w.x & kEntV) lds_add(acc, w.x & 0xFFFFu, __hiloint2double((int)w.z, (int)w.y) * ra);
 }
+// data unit q of a dense V row's run: columns 2q and 2q + 1 (zero values skipped)
+__device__ __forceinline__ void add_unit_d(double *acc, uint4 w, int q, double ra) {
+  const double a = __hiloint2double((int)w.y, (int)w.x), b = __hiloint2double((int)w.w, (int)w.z);
+  if (a != 0.0) lds_add(acc, (uint32_t)(2 * q), a * ra);
+  if (b != 0.0) lds_add(acc, (uint32_t)(2 * q + 1), b * ra);
+}
 
 // Fast decode (P rows whose classes are all < kInvTab): s_inv sits at LDS address 0.
 __device__ __forceinline__ void add_slot_fast(double *acc, uint32_t s, double ra,
@@ -1578,9 +1632,12 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (t0 + j >= nov) continue;
-          const uint32_t n = (uint32_t)__shfl((int)y4[j].x, 0);
+          const uint32_t n0 = (uint32_t)__shfl((int)y4[j].x, 0);
+          const bool dn = (n0 & kRunDense) != 0;  // (a dense V row: unit q -> columns 2q, 2q+1)
+          const uint32_t n = n0 & ~kRunDense;
           if (lane == 0 || (uint32_t)lane > n) y4[j] = uint4{0u, 0u, 0u, 0u};
-          if (v4[j]) add_unit_v(acc, y4[j], r4[j]);
+          if (dn) add_unit_d(acc, y4[j], lane - 1, r4[j]);
+          else if (v4[j]) add_unit_v(acc, y4[j], r4[j]);
           else add_unit(acc, y4[j], false, r4[j], s_inv, a.g_inv);
           // runs longer than 63 units (hub items' V rows: up to a whole tile of entries): 4
           // chunks of 64 units in flight per round instead of one load -> add at a time
@@ -1594,7 +1651,8 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
               if (c + 64 * p > n) break;  // (uniform)
-              if (v4[j]) add_unit_v(acc, z[p], r4[j]);
+              if (dn) add_unit_d(acc, z[p], (int)(c + 64 * p) + lane - 1, r4[j]);
+              else if (v4[j]) add_unit_v(acc, z[p], r4[j]);
               else add_unit(acc, z[p], false, r4[j], s_inv, a.g_inv);
             }
           }

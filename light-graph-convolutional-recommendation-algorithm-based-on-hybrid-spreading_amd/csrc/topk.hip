@@ -451,6 +451,9 @@ __device__ unsigned long long g_topk_counts[16];
 #ifndef LG_RING_NG
 #define LG_RING_NG 2
 #endif
+#ifndef LG_RING_W  // waves per block at k <= 32 (default: 256 users per block)
+#define LG_RING_W (16 / LG_RING_NG)
+#endif
 
 // the fragment ring's chunk: 8 KiB for 8 waves (64 items at d = 64), 4 or 8 KiB for 4; other
 // wave counts (measurement shapes): the smallest multiple of one 16-byte piece per thread of
@@ -1476,6 +1479,15 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
 #ifndef LG_TOPK_GL32
 #define LG_TOPK_GL32 0
 #endif
+#ifndef LG_SEED4_NG  // the k > 32 seed pass's shape
+#define LG_SEED4_NG 1
+#endif
+#ifndef LG_SEED4_NBUF
+#define LG_SEED4_NBUF 9
+#endif
+#ifndef LG_SEED4_LA
+#define LG_SEED4_LA 5
+#endif
 #ifndef LG_GL_NG  // user groups per wave in the GL shapes (4: 512 users per block)
 #define LG_GL_NG 2
 #endif
@@ -1517,23 +1529,23 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
   } else if (gm == 4) {
     LG_RING_LAUNCH(LG_GL_NG, 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
   } else if (M == 1 && seedp) {
-    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
+    LG_RING_LAUNCH(LG_RING_NG, LG_RING_W, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
                    LG_RING_LAG, true, false)
   } else if (M == 1) {
-    LG_RING_LAUNCH(LG_RING_NG, 16 / LG_RING_NG, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
+    LG_RING_LAUNCH(LG_RING_NG, LG_RING_W, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
                    LG_RING_LAG, false, false)
   } else if (M == 2 && seedp) {
     LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, true, false)
   } else if (M == 2) {
     if (LG_TOPK_LDS_LISTS)
       LG_RING_LAUNCH(1, 8, 2, LG_RING2_CAP, LG_RING2_NBUF, LG_RING_LA, LG_RING_LAG, false, false)
+  } else if (seedp) {
+    // (k > 32: the seed pass keeps no lists, so its ring takes the LDS the lists would)
+    LG_RING_LAUNCH(LG_SEED4_NG, 8, 4, 160, LG_SEED4_NBUF, LG_SEED4_LA, 1, true, false)
   } else if constexpr (D > 64) {  // (the LG_RING4_* shapes apply to d <= 64)
-    if (seedp) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, true, false)
-    else if (LG_TOPK_LDS_LISTS) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, false, false)
+    if (LG_TOPK_LDS_LISTS) LG_RING_LAUNCH(1, 8, 4, 160, 4, 2, 1, false, false)
   } else {
-    if (seedp)
-      LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, true, false)
-    else if (LG_TOPK_LDS_LISTS)
+    if (LG_TOPK_LDS_LISTS)
       LG_RING_LAUNCH(1, LG_RING4_W, 4, LG_RING4_CAP, LG_RING4_NBUF, LG_RING4_LA, 1, false, false)
   }
 #undef LG_RING_LAUNCH

@@ -679,11 +679,21 @@ class TileWeights:
             isv, has, slow, ou = h >> 31, (h >> 30) & 1, (h >> 29) & 1, h & 0x1FFFFFFF
             assert bool(isv) == bool(hub[i]) and (slow or not isv)
             run = np.zeros((0, 4), np.uint32)
-            if has:
+            if has and not (isv and int(ovf[4 * ou]) >> 31):
                 n = int(ovf[4 * ou])
                 assert np.all(ovf[4 * ou + 1:4 * ou + 4] == 0)
                 run = ovf[4 * (ou + 1):4 * (ou + 1 + n)].reshape(n, 4)
+            if isv and has and int(ovf[4 * ou]) >> 31:  # a dense V row
+                nd = int(ovf[4 * ou]) & 0x7FFFFFFF
+                assert nd == (self.width + 1) // 2 and np.all(lines[i, 1:] == 0)
+                run = ovf[4 * (ou + 1):4 * (ou + 1 + nd)].reshape(nd, 4)
+                vals = run.reshape(-1).view(np.uint64).view(np.float64)  # (lo, hi) pairs
+                assert np.all(vals[self.width:] == 0) and int((vals != 0).sum()) == rl[i]
+                assert rl[i] > self.width // 2 + 8
+                out[i, :] = vals[:self.width]
+                continue
             if isv:
+                assert rl[i] <= self.width // 2 + 8
                 assert np.all(lines[i, 1:4] == 0)
                 units = np.concatenate([lines[i, 4:].reshape(7, 4), run])
                 units = units[units[:, 0] != 0]
@@ -814,6 +824,9 @@ class TileWeights:
             self.paths_read += (self.row_uses * ln).sum()
             self.paths_hub += (self.row_uses * ln * hub[:I]).sum()  # (V rows' share)
             used = _run_units(ln, hub)
+            # (dense V rows: ceil(width / 2) data units + the header, whatever their entries)
+            used = torch.where(hub[:I] & (ln > self.width // 2 + 8),
+                               torch.full_like(used, 1 + (self.width + 1) // 2), used)
             self.bytes_read += 128 * self.row_uses.sum() + 16 * (self.row_uses * used).sum()
 
 def spread_topk_tiled(A: Interactions, lam: float, k: int, excl: RowSets | None,

@@ -42,7 +42,7 @@ class PerTileWeights(ops.TileWeights):
         N.ref_check(R.lg_spread_tile_rows_f64(
             N.ptr(A.by_item.rowptr), N.ptr(A.by_item.col), N.ptr(A.by_user.col),
             N.ptr(self.user_cls), N.ptr(self.inv_deg), I, N.ptr(self.cur), N.ptr(self.count1),
-            j0, self.tile, N.ptr(self.g_bound), self.vthr, N.ptr(ovf_ptr), N.ptr(self.g_lines),
+            j0, widths[0], N.ptr(self.g_bound), self.vthr, N.ptr(ovf_ptr), N.ptr(self.g_lines),
             N.ptr(self.g_ovf), N.ptr(self.g_row_len), N.ptr(self.ws), self.ws.numel(), strm),
             "lg_spread_tile_rows_f64")
         self._grp = (j0, widths, [0], [total])

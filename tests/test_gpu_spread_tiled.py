@@ -336,7 +336,8 @@ def test_spread_stats_count_path_updates(fused):
     the item range: a P row holds one slot per (user, item) pair behind it (the co-occurrence
     counts of the row, A^T A), a hub row (more pairs than the tile width) one entry per
     distinct column; stats["w_bytes"] = 128 bytes per (user, item, tile) line plus 16 per
-    overflow unit (run header + data)."""
+    overflow unit (run header + data; a dense hub row -- more than width / 2 + 8 entries --
+    ceil(width / 2) data units)."""
     from lgcnhs import ops
     U, I = 150, 400
     A = _inter(U, I, 3000, seed=3, zipf=True)
@@ -360,6 +361,8 @@ def test_spread_stats_count_path_updates(fused):
             ln = np.where(hub, (blk != 0).sum(1), pairs)
             units = np.where(hub, np.where(ln > 7, 1 + ln - 7, 0),
                              np.where(ln > 31, 1 + (ln - 31 + 3) // 4, 0))
+            w = blk.shape[1]
+            units = np.where(hub & (ln > w // 2 + 8), 1 + (w + 1) // 2, units)
             paths += int((uses * ln).sum())
             nbytes += int((uses * (128 + 16 * units)).sum())
         assert st["w_paths"] == paths
