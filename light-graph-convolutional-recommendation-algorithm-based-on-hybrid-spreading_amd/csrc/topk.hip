@@ -322,6 +322,14 @@ __device__ __forceinline__ float next_below(float x) {
   return __builtin_bit_cast(float, x > 0.f ? b - 1 : b + 1);
 }
 
+// a float at or below t - m (finite t and m: fl(t - m) moved one ulp down; t = +-inf stays; NaN
+// m gives NaN)
+__device__ __forceinline__ float thr_minus(float t, float m) {
+  const float d = t - m;
+  if (!(d > -__builtin_huge_valf() && d < __builtin_huge_valf())) return d;
+  return next_below(d);
+}
+
 // K2r: the screened top-K (every k <= 128), with bound-side lists -- no exact score inside
 // the streaming loop. A bf16 MFMA product (v_mfma_f32_16x16x32_bf16, 16x the f32 MFMA's rate)
 // plus a rigorous per-user margin m_u (umarg, include/lgcnhs.h: |G_bf16 - G_chain| <= m_u for
@@ -419,6 +427,9 @@ __device__ unsigned long long g_topk_counts[16];
 // users x CAP x 6 B + NBUF x 8 KiB + 2 KiB within 160 KiB.
 #ifndef LG_RING_CAP
 #define LG_RING_CAP 56
+#endif
+#ifndef LG_RING_LEAN  // the leaner ring check and chunk test (-DLG_RING_LEAN=0: round 5's)
+#define LG_RING_LEAN 1  // (C5 k = 20: 9.05 -> 8.89 ms, k = 100: 16.85 -> 16.72 ms)
 #endif
 #ifndef LG_RING_NBUF
 #define LG_RING_NBUF 9
@@ -535,6 +546,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
   int cnt[NG], chk[NG];
   int gcnt[NG];  // (GL) entries in the user's slab; chk: its count at the last compaction
   float thr[NG];
+  // LG_RING_LEAN: the chunk test's threshold on the product itself, at or below thr - marg
+  // (a product b with fl(b + m) > thr has b >= thr - m >= thrm; NaN margins give NaN: every
+  // chunk hits), kept with thr
+  float thrm[NG];
   float sthr[NG];  // the seeded floor of the threshold (-inf without a seed)
   // the entry threshold over a list's k-th lower bound tau and the seed floor st: an
   // excluded item ranks at the mask value, so while that reaches the floor anything enters
@@ -575,6 +590,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     chk[g] = 0;
     gcnt[g] = 0;
     thr[g] = uvalid[g] ? entry_thr(neg_inf<float>(), sthr[g]) : __builtin_huge_valf();
+    thrm[g] = thr_minus(thr[g], marg[g]);
   }
   // (GL) the slab of user u of group g (valid users only: padding users never insert)
   auto gslab = [&](int g, int u) __attribute__((always_inline)) {
@@ -833,6 +849,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
         chk[j] = nk;
         ex_pos[j] = pos;
         thr[j] = uvalid[j] ? nthr : __builtin_huge_valf();
+        thrm[j] = thr_minus(thr[j], marg[j]);
       }
   };
   // compact every list that could overflow on the next tile (+16 entries max per tile)
@@ -1002,8 +1019,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
     };
     // every wave's count (bits `sh`) has reached `need` (16-bit wrap-around)
     auto all_reached = [&](uint32_t v, uint32_t need, int sh) __attribute__((always_inline)) {
+#if LG_RING_LEAN
+      // (bit 15 of the 16-bit difference = not yet reached; the ballot masked by a constant
+      // instead of a per-lane condition: one compare, no select)
+      const uint64_t nr = __ballot((((v >> sh) - need) & 0x8000u) != 0u);
+      return (nr & ((WAVES >= 64 ? 0ull : (1ull << WAVES)) - 1ull)) == 0;
+#else
       const int16_t d = (int16_t)(uint16_t)(((v >> sh) - need) & 0xffffu);
       return __ballot(lane < WAVES && d < 0) == 0;
+#endif
     };
     auto wait_reached = [&](uint32_t &v, uint32_t need, int sh) __attribute__((always_inline)) {
       while (!all_reached(v, need, sh)) {
@@ -1047,6 +1071,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
       uint32_t gm = 0;
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
+#if LG_RING_LEAN
+        // a linear chain folds two values per v_maximum3_f32 (the pairwise tree left one of
+        // every other instruction's three inputs duplicated)
+        float m = acc[0][g][0];
+#pragma unroll
+        for (int e = 1; e < 4 * TPC; ++e)
+          m = __builtin_elementwise_maximum(m, acc[e / 4][g][e % 4]);
+#else
         float m = max4(acc[0][g]);
 #pragma unroll
         for (int tt = 1; tt < TPC; ++tt)
@@ -1054,7 +1086,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_topk_ring(
               m, __builtin_elementwise_maximum(
                      __builtin_elementwise_maximum(acc[tt][g][0], acc[tt][g][1]),
                      __builtin_elementwise_maximum(acc[tt][g][2], acc[tt][g][3])));
+#endif
+#if LG_RING_LEAN
+        if (__ballot(!(m < thrm[g])) != 0) gm |= 1u << g;  // (thrm: below)
+#else
         if (__ballot(above(m + marg[g], thr[g])) != 0) gm |= 1u << g;
+#endif
       }
       return gm;
     };

@@ -22,7 +22,7 @@ from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 USERS, ITEMS, K = 32768, 1_000_000, 20
-PAT = r"k_topk_ring<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, \d+, (true|false)>"
+PAT = r"k_topk_ring<(\d+), (\d+), (\d+), \d+, \d+, \d+, \d+, \d+, (true|false)(?:, (?:true|false))?>"
 
 
 def main(tag, d, K=K):
