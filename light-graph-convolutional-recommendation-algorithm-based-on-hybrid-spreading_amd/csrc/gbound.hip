@@ -56,6 +56,54 @@ __device__ __forceinline__ float row_max4(float m) {
   return fmaxf(__builtin_bit_cast(float, x), __builtin_bit_cast(float, y));
 }
 
+// Half exchanges over the 16-lane rows (gfx950): v_permlane32_swap x, y -- rows 2-3 of x <->
+// rows 0-1 of y; v_permlane16_swap x, y -- rows 1, 3 of x <-> rows 0, 2 of y. Inline asm with
+// the waits inside: 2 wait states between a VALU write and a swap reading it, and between a
+// swap and a VALU reading its result (hipcc's builtins pad the first only: a value read right
+// after its swap came out wrong on the box, the last chunk's q bytes in
+// test_score_bounds_cover_chain_scores_many_blocks).
+__device__ __forceinline__ void swap32x2(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3\n\t"
+               "s_nop 1" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void swap16x2(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+               "s_nop 1" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void swap16(uint32_t &a, uint32_t &b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+
+// 4 x 4 transpose of (register t, lane row): afterwards row r's register t holds what row t's
+// register r held
+__device__ __forceinline__ void rows_transpose(uint32_t w[4]) {
+  asm volatile("s_nop 1\n\t"
+               "v_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3\n\t"
+               "s_nop 1\n\t"
+               "v_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+               "s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+}
+
+// maximum of two floats given as bits (v_maximum_f32: a NaN propagates)
+__device__ __forceinline__ float fmax_bits(uint32_t a, uint32_t b) {
+  return __builtin_elementwise_maximum(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
+}
+
+// u, v hold at lane row kg the value of group P(kg) = {0, 2, 1, 3}[kg] (of the lane's
+// column); ou[g], ov[g] = group g's values on every row
+__device__ __forceinline__ void rows_broadcast2(float u, float v, float ou[4], float ov[4]) {
+  uint32_t x = __builtin_bit_cast(uint32_t, u), y = x;
+  uint32_t p = __builtin_bit_cast(uint32_t, v), q = p;
+  swap16x2(x, y, p, q);  // x = [u0 u0 u1 u1], y = [u2 u2 u3 u3] (p, q likewise)
+  uint32_t x2 = x, y2 = y, p2 = p, q2 = q;
+  swap32x2(x, x2, y, y2);
+  swap32x2(p, p2, q, q2);
+  ou[0] = __builtin_bit_cast(float, x), ou[1] = __builtin_bit_cast(float, x2);
+  ou[2] = __builtin_bit_cast(float, y), ou[3] = __builtin_bit_cast(float, y2);
+  ov[0] = __builtin_bit_cast(float, p), ov[1] = __builtin_bit_cast(float, p2);
+  ov[2] = __builtin_bit_cast(float, q), ov[3] = __builtin_bit_cast(float, q2);
+}
+
 __device__ __forceinline__ float round_up_f32(double x) {
   float f = (float)x;
   if ((double)f < x) f = nextafterf(f, __builtin_huge_valf());
@@ -143,6 +191,33 @@ __global__ __launch_bounds__(256) void k_bound_prep4(const float *__restrict__ x
 // hands it over -- a quarter of the L2 fragment reads, and their latency hidden by a whole
 // chunk of work. W = waves per SIMD the registers and LDS are sized for (D <= 64: 3, D = 128:
 // 2). Waves past the last user still load and synchronise (their stores are masked).
+// s_waitcnt vmcnt(n) for a uniform run-time n <= K (the count is an immediate: a chain of
+// scalar compares picks the instruction)
+template <int K>
+__device__ __forceinline__ void vm_wait_le(int n) {
+  if constexpr (K > 0) {
+    if (n < K) {
+      vm_wait_le<K - 1>(n);
+      return;
+    }
+  }
+  static_assert(K <= 63, "vmcnt holds 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K) : "memory");
+}
+
+// chunk buffers of the score-bound kernel's ring (D = 128: 4 x 16 KB, 2 blocks per CU)
+#ifndef LG_BOUND_NB
+#define LG_BOUND_NB(D) ((D) <= 64 ? 5 : 4)
+#endif
+
+// cache-policy bits of the q and gb stores: nt (streaming; 0.84 -> 0.75 ms per C5 tile for
+// the q stores, scripts/micro_bound.py)
+#ifndef LG_QSTORE_AUX
+#define LG_QSTORE_AUX 2
+#endif
+#ifndef LG_GB_AUX
+#define LG_GB_AUX 0
+#endif
 template <int D, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void k_chunk_bound(const __bf16 *__restrict__ ub,
                                                      const float *__restrict__ unorm,
@@ -168,12 +243,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       bfr[g][s] = *reinterpret_cast<const bf16x8 *>(ub + uu * D + 32 * s + 8 * kg);
     un[g] = unorm[uu];
   }
-  // q bytes of two chunks (64 users x 128 columns) staged in LDS, then written as whole
-  // 128-byte row segments (8 lanes x 16 bytes per user); 16-byte groups of a row swizzled by
-  // the row (2-way bank conflicts at most on the dword writes)
-  constexpr int QS = 32;  // dwords per user row
-  __shared__ __attribute__((aligned(16))) uint32_t qs_all[4][64 * QS];
-  uint32_t *qs = qs_all[wv];
   // the staged chunks: 64 item rows of D bf16 (2 D bytes), written by LDS-DMA
   // (global_load_lds_dwordx4: each wave instruction fills 1 KB contiguously, no VGPRs); the
   // 16-byte pieces of row r sit XOR-swizzled by sw(r) = (r / (128 / D)) & (D / 8 - 1), so the
@@ -182,22 +251,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   constexpr int RB = 2 * D;               // bytes per staged row
   constexpr int NL = 64 * PR / 256;       // DMA instructions per thread per chunk (D = 32: 1)
   static_assert(NL >= 1 && 64 * PR % 256 == 0, "chunk pieces must spread over the block");
-  __shared__ __attribute__((aligned(16))) char frs[2][64 * RB];
+  // a ring of NB chunk buffers: chunk c + NB - 1's DMA goes out while chunk c is computed, so
+  // the wait at a chunk's end (for chunk c + 1) leaves the stores of the last NB - 1 chunks in
+  // flight -- vmcnt completes in issue order, and with 2 buffers every chunk waited for the
+  // previous chunk's q stores to be acknowledged (the q bytes' write latency then set the
+  // pace: 0.74 ms per C5 tile with 3 buffers, 0.24 without q)
+  constexpr int NB = LG_BOUND_NB(D);
+  __shared__ __attribute__((aligned(16))) char frs[NB][64 * RB];
   auto sw = [](int r) { return (r / (128 / D)) & (PR - 1); };
-  auto dma = [&](int cb, int buf) __attribute__((always_inline)) {
+  // per thread and DMA instruction j: the chunk row of its piece and the piece's byte offset
+  // from the chunk's first item row (loop-invariant; the chunk's base address is uniform and
+  // goes in the instruction's SGPR pair)
+  int drow[NL];
+  uint32_t doff[NL];
 #pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int p = 256 * j + 64 * wv + lane;
+    drow[j] = p / PR;
+    doff[j] = (uint32_t)(2 * (drow[j] * D + 8 * ((p % PR) ^ sw(drow[j]))));
+  }
+  auto dma = [&](int cb, int buf) __attribute__((always_inline)) {
+    const __bf16 *base = ib + (int64_t)(item_begin + cb) * D;
+    const bool part = cb + 64 > width;  // a partial last chunk: rows past the width re-read
+#pragma unroll                          // the tile's last item
     for (int j = 0; j < NL; ++j) {
-      const int u0 = 256 * j + 64 * wv;  // the wave's first 16-byte unit of this instruction
-      const int p = u0 + lane, r = p / PR;
-      int it = cb + r;
-      it = it < width ? it : width - 1;
-      const __bf16 *src = ib + (int64_t)(item_begin + it) * D + 8 * ((p % PR) ^ sw(r));
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(frs[buf] + 16 * u0));
+      uint32_t off = doff[j];
+      if (part) {
+        const int rr = drow[j] < width - cb ? drow[j] : width - 1 - cb;
+        off -= (uint32_t)(2 * D * (drow[j] - rr));
+      }
+      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(
+          __attribute__((address_space(3))) char *)(frs[buf] + 16 * (256 * j + 64 * wv)));
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(off), "s"(base), "s"(dst) : "memory");
     }
   };
   // the wave's 64 rows of gb through one descriptor (32-bit offsets)
@@ -205,6 +293,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   const __amdgpu_buffer_rsrc_t rgb = __builtin_amdgcn_make_buffer_rsrc(
       (void *)(gb + (ubase < n_users ? ubase : 0) * nch), 0,
       nrow_w > 0 ? (int)(nrow_w * nch * 4) : 0, 0x00020000);
+  // the wave's 64 q rows through one descriptor (rows past n_users are out of range: their
+  // stores are dropped), 32-bit offsets
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      qb ? (void *)(qb + (ubase < n_users ? ubase : 0) * (int64_t)qstride) : nullptr, 0,
+      qb && nrow_w > 0 ? (int)(nrow_w * qstride) : 0, 0x00020000);
   // every chunk's largest item norm (the margin's ||j|| factor), once per block: wave w folds
   // chunks w, w + 4, ... (the loads first, then the reductions side by side)
   __shared__ float s_cmax[kBoundMaxWidth / 64];
@@ -225,10 +318,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       if (lane == 0) s_cmax[wv + 4 * k] = m;
     }
   }
-  dma(0, 0);
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+    if (j < nch) dma(64 * j, j);
   // the DMA is inline asm, invisible to hipcc's waits: this wave's copies have landed only
   // after an explicit vmcnt wait, which must precede the barrier that publishes the buffer
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (the later chunks' copies may stay in flight)
+  vm_wait_le<NL * (NB - 2)>(NL * ((nch < NB - 1 ? nch : NB - 1) - 1));
   __syncthreads();
   // every prologue load (the user fragments and norms above) is taken here, before the loop:
   // a load still pending at the loop head gets its wait inside the loop, where it also drains
@@ -239,17 +335,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     for (int s = 0; s < S; ++s) asm volatile("" : "+v"(bfr[g][s]));
     asm volatile("" : "+v"(un[g]));
   }
+  // lane row kg reduces and stores the bound of user group P(kg) = {0, 2, 1, 3}[kg] (the row
+  // exchanges below leave the groups in that order)
+  const float unl = kg == 0 ? un[0] : kg == 1 ? un[2] : kg == 2 ? un[1] : un[3];
+  const uint32_t gbo = (uint32_t)(4 * (16 * (kg == 1 ? 2 : kg == 2 ? 1 : kg) + ul) * nch);
+  // q: user 16 g + ul's row, lane row kg's 16 columns (all in the VGPR offset, which the
+  // descriptor's range check covers: rows past n_users are dropped). The SGPR offset stays 0:
+  // with a register there hipcc does not pad the 16-byte store's data hazard (a VALU writing
+  // the data registers right after the store), and on the box such an overwrite reached the
+  // store (q bytes of lanes 12-15 of every row wrong, the last chunk's second dword)
+  uint32_t qo[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) qo[g] = (uint32_t)((16 * g + ul) * qstride + 16 * kg);
+  // gb: the lane's user's bounds of 8 consecutive chunks are collected in registers (a shift
+  // register, gq[7] the latest) and leave as 32 contiguous bytes -- one dword store per chunk
+  // wrote each 32-byte memory sector 8 times over (WRITE_SIZE 1.2 GB per C5 tile for 128 MB
+  // of bounds)
+  float gq[8];
   // the vector-memory operations each chunk issues after its DMA (the loop issues no loads):
-  // one gb store per user group, and on a chunk pair's second chunk one 16-byte q store per
-  // 8 users -- the waits at the loop's end leave exactly these in flight (below)
-  constexpr int kGbStores = 4;  // the `g` loop's raw_buffer_store_b32
-  constexpr int kQStores = 8;   // the `r8` loop's raw_buffer_store_b128
+  // with q one 16-byte q store per lane and user group -- the waits at the loop's end leave
+  // these in flight (below); the gb stores of every 8th chunk are not counted, so the wait
+  // after them is stricter than it needs to be, never looser
+  constexpr int kQStores = 4;   // the `g` loop's raw_buffer_store_b128
   for (int c = 0; c < nch; ++c) {
     const int cb = 64 * c;  // chunk start inside the tile
-    if (c + 1 < nch)
-      dma(cb + 64, (c + 1) & 1);  // into the buffer every wave finished reading at the last barrier
+    if (c + NB - 1 < nch)  // into the buffer every wave finished reading at the last barrier
+      dma(cb + 64 * (NB - 1), (c + NB - 1) % NB);
     const float inm = s_cmax[c];  // the chunk's largest item norm
-    float gmax[4];
     f32x4 accs[4][4];  // [item tile t][user group g]
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -257,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       bf16x8 fa[S];
 #pragma unroll
       for (int s = 0; s < S; ++s)
-        fa[s] = *reinterpret_cast<const bf16x8 *>(frs[c & 1] + (16 * t + ul) * RB +
+        fa[s] = *reinterpret_cast<const bf16x8 *>(frs[c % NB] + (16 * t + ul) * RB +
                                                   16 * ((4 * s + kg) ^ sw(16 * t + ul)));
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -279,94 +391,105 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 #pragma unroll
             for (int g = 0; g < 4; ++g) accs[t][g][r] = -__builtin_huge_valf();
     }
+    // the lane's maximum per group (16 scores), then over the 4 lane rows for all groups at
+    // once: row exchanges pair rows 0 <-> 2, 1 <-> 3 of groups 0 and 1 (2 and 3) in one
+    // maximum, then rows 0 <-> 1 across the pairs -- row kg ends with group P(kg)'s maximum
+    uint32_t gm[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      float m = max3f(accs[0][g][0], accs[0][g][1], accs[0][g][2]);
-      m = max3f(m, accs[0][g][3], accs[1][g][0]);
-      m = max3f(m, accs[1][g][1], accs[1][g][2]);
-      m = max3f(m, accs[1][g][3], accs[2][g][0]);
-      m = max3f(m, accs[2][g][1], accs[2][g][2]);
-      m = max3f(m, accs[2][g][3], accs[3][g][0]);
-      m = max3f(m, accs[3][g][1], accs[3][g][2]);
-      gmax[g] = __builtin_elementwise_maximum(m, accs[3][g][3]);
+      const float m0 = max3f(accs[0][g][0], accs[0][g][1], accs[0][g][2]);
+      const float m1 = max3f(accs[0][g][3], accs[1][g][0], accs[1][g][1]);
+      const float m2 = max3f(accs[1][g][2], accs[1][g][3], accs[2][g][0]);
+      const float m3 = max3f(accs[2][g][1], accs[2][g][2], accs[2][g][3]);
+      const float m4 = max3f(accs[3][g][0], accs[3][g][1], accs[3][g][2]);
+      gm[g] = __builtin_bit_cast(
+          uint32_t, __builtin_elementwise_maximum(max3f(m0, m1, m2), max3f(m3, m4, accs[3][g][3])));
     }
-    static_assert(kGbStores == 4, "one gb store per group g below");
+    swap32x2(gm[0], gm[1], gm[2], gm[3]);
+    uint32_t ma = __builtin_bit_cast(uint32_t, fmax_bits(gm[0], gm[1]));
+    uint32_t mb = __builtin_bit_cast(uint32_t, fmax_bits(gm[2], gm[3]));
+    swap16(ma, mb);
+    const float m = fmax_bits(ma, mb);
+    const float marg = kBoundMargin * unl * inm;
+    float b = m + marg;
+    b += fabsf(b) * 0x1p-22f + 1e-30f;
+    b = b == b ? b : __builtin_huge_valf();  // NaN (a non-finite score): no bound, +inf
+    // (every lane stores; rows past n_users fall outside the descriptor's range and are
+    // dropped; the chunk goes in the VGPR offset, see qo below)
 #pragma unroll
-    for (int g = 0; g < kGbStores; ++g) {
-      const float m = row_max4(gmax[g]);
-      const float marg = kBoundMargin * un[g] * inm;
-      float b = m + marg;
-      b += fabsf(b) * 0x1p-22f + 1e-30f;
-      // every lane stores (one store per wave and group, not a branch that hipcc's waits
-      // would have to count as possibly skipped): lanes kg > 0 and rows past n_users fall
-      // outside the descriptor's range and are dropped
-      __builtin_amdgcn_raw_buffer_store_b32(
-          __builtin_bit_cast(uint32_t, b), rgb,
-          kg == 0 ? (uint32_t)(4 * ((16 * g + ul) * nch + c)) : 0x7FFFFFF0u, 0, 0);
-      if (qb) {
-        // per column: q = rne(v') with v' = fl(acc sc + msc) >= 255 (acc + marg) / b + 0.5 (sc
-        // and msc carry (1 + 2^-20) factors over their own roundings and the fma's; msc holds
-        // the 0.5 plus 1e-4 for the fma's absolute rounding near 0), so q >= the ratio; the
-        // conversion saturates to [0, 255]; 4 consecutive items of one user per lane and
-        // tile -> one dword
-        const float sc = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) * (1.f + 0x1p-20f) : 0.f;
-        const float msc = (marg * sc * (1.f + 0x1p-20f) + 0.5001f) * (1.f + 0x1p-20f);
+    for (int k = 0; k < 7; ++k) gq[k] = gq[k + 1];
+    gq[7] = b;
+    if ((c & 7) == 7) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, (f32x4){gq[0], gq[1], gq[2], gq[3]}), rgb,
+          gbo + 4 * (c - 7), 0, LG_GB_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, (f32x4){gq[4], gq[5], gq[6], gq[7]}), rgb,
+          gbo + 4 * (c - 3), 0, LG_GB_AUX);
+    } else if (c + 1 == nch) {  // the last chunk: the held bounds of chunks c - (c & 7) .. c
+#pragma unroll
+      for (int k = 0; k < 7; ++k)
+        if (k >= 7 - (c & 7))
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gq[k]), rgb,
+                                                gbo + 4 * (c - 7 + k), 0, LG_GB_AUX);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gq[7]), rgb, gbo + 4 * c,
+                                            0, LG_GB_AUX);
+    }
+    if (qb) {
+      // per column: q = rne(v') with v' = fl(acc sc + msc) >= 255 (acc + marg) / b + 0.5 (sc
+      // and msc carry (1 + 2^-20) factors over their own roundings and the fma's; msc holds
+      // the 0.5 plus 1e-4 for the fma's absolute rounding near 0), so q >= the ratio; the
+      // conversion saturates to [0, 255]. sc and msc are the lane row's group's; row
+      // exchanges hand every group's pair to all 4 rows
+      const float scl = b > 0.f ? 255.f / b * (1.f + 0x1p-20f) * (1.f + 0x1p-20f) : 0.f;
+      const float mscl = (marg * scl * (1.f + 0x1p-20f) + 0.5001f) * (1.f + 0x1p-20f);
+      float sc[4], msc[4];
+      rows_broadcast2(scl, mscl, sc, msc);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        // 4 consecutive items of one user per lane and tile -> one dword w[t] (lane row kg:
+        // items 16 t + 4 kg .. + 3)
+        // (the fma on pairs: v_pk_fma_f32, two columns per instruction, the same roundings)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 s2 = {sc[g], sc[g]}, m2 = {msc[g], msc[g]};
+        uint32_t w[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          // (scalar v_fma_f32; the packed v_pk_fma_f32 form measured the same, 0.805 vs 0.808 ms
-          // per C5 tile)
-          float v[4];
+          const f32x2 lo = __builtin_elementwise_fma(
+              (f32x2){accs[t][g][0], accs[t][g][1]}, s2, m2);
+          const f32x2 hi = __builtin_elementwise_fma(
+              (f32x2){accs[t][g][2], accs[t][g][3]}, s2, m2);
+          const float v[4] = {lo[0], lo[1], hi[0], hi[1]};
+          w[t] = 0;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(accs[t][g][r], sc, msc);
-          uint32_t w = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) w = __builtin_amdgcn_cvt_pk_u8_f32(v[r], r, w);
-          // user 16 g + ul, columns (c & 1) * 64 + 16 t + 4 kg of the pair (16-byte group
-          // 4 (c & 1) + t, swizzled by the row)
-          const int row = 16 * g + ul;
-          qs[row * QS + 4 * ((4 * (c & 1) + t) ^ (row & 7)) + kg] = w;
+          for (int r = 0; r < 4; ++r) w[t] = __builtin_amdgcn_cvt_pk_u8_f32(v[r], r, w[t]);
         }
-      }
-    }
-    const bool pair = qb && ((c & 1) || c + 1 == nch);
-    if (pair) {  // a chunk pair is complete: write it out
-      wave_sync();
-      const int cp = 64 * (c & ~1);  // the pair's first column (its 128 columns fit qstride)
-      // the wave's 64 q rows through one descriptor (rows past n_users are out of range:
-      // their stores are dropped), 32-bit offsets
-      const int64_t nrow = n_users - ubase < 64 ? n_users - ubase : 64;
-      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(qb + (ubase < n_users ? ubase : 0) * qstride), 0,
-          nrow > 0 ? (int)(nrow * qstride) : 0, 0x00020000);
-#pragma unroll
-      for (int r8 = 0; r8 < kQStores; ++r8) {  // (every lane stores: no store is conditional)
-        const int uloc = 8 * r8 + (lane >> 3);
-        const uint4 v =
-            *reinterpret_cast<const uint4 *>(qs + uloc * QS + 4 * ((lane & 7) ^ (uloc & 7)));
-#ifdef LG_QBLOCKED  // measurement: the wave's 64 rows of a chunk pair as one 8 KB block
-        const uint32_t qo = (uint32_t)((cp / 128) * nrow * 128 + uloc * 128 + 16 * (lane & 7));
-#else
-        const uint32_t qo = (uint32_t)(uloc * qstride + cp + 16 * (lane & 7));
-#endif
+        // 4 x 4 transpose of (tile t, lane row kg): lane row kg then holds tile kg's 16
+        // consecutive columns, w[0..3] = its 4 dwords in order
+        rows_transpose(w);
+        // user 16 g + ul, columns cb + 16 kg .. + 15: 16 users x 64 contiguous bytes per
+        // store (every lane stores; a partial last chunk's columns past the width land in
+        // the row's padding, qstride >= the width rounded up to 256)
         __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rq, qo, 0, 0);
+            (__attribute__((ext_vector_type(4))) uint32_t){w[0], w[1], w[2], w[3]}, rq,
+            qo[g] + cb, 0, LG_QSTORE_AUX);
       }
-      wave_sync();
     }
     // chunk c + 1's DMA (this wave's share) landed, then the barrier publishes the buffer.
-    // vmcnt counts stores as well, and completes in issue order: the wait leaves this chunk's
-    // kGbStores gb stores and the pair's kQStores q stores (issued after the DMA, no loads in
-    // the loop) in flight -- a vmcnt(0) here would wait for every store to reach L2 once per
-    // chunk. The counts are the unconditional store loops above (every lane issues every
-    // store; a store made conditional or merged would have to change them); the last chunk
-    // waits for everything.
-    if (c + 1 == nch)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (pair)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kGbStores + kQStores) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kGbStores) : "memory");
-    __syncthreads();
+    // vmcnt counts stores as well, and completes in issue order: the wait leaves in flight
+    // what was issued after that DMA (it went out in chunk c + 2 - NB, or in the prologue) --
+    // the q stores of chunks max(0, c + 2 - NB) .. c and the DMAs of chunks c + 2 ..
+    // min(c + NB - 1, nch - 1). kQStores per chunk: the unconditional store statements above
+    // (every lane issues every store; a store made conditional or merged would have to change
+    // the count); the gb stores are not counted (stricter, never looser). The last chunk
+    // waits for nothing: the kernel ends.
+    if (c + 1 < nch) {
+      const int nst = (qb ? kQStores : 0) * (c + 1 < NB - 1 ? c + 1 : NB - 1);
+      const int ndma = NL * (nch - 2 - c < NB - 2 ? nch - 2 - c : NB - 2);
+      vm_wait_le<kQStores * (NB - 1) + NL * (NB - 2)>(nst + ndma);
+      __syncthreads();
+    }
   }
 }
 

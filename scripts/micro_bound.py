@@ -55,8 +55,33 @@ def fill(r=0):
     q.fill_(r & 255)
 
 
+def strided(piece):
+    # the q bytes written piece by piece: every row's `piece` bytes of one column block, then the
+    # next block (the kernel's write pattern: at a time, one chunk of many users' rows)
+    v = q.view(a.users, T // piece, piece)
+
+    def f(r=0):
+        for c in range(T // piece):
+            v[:, c].fill_(r & 255)
+    return f
+
+
+def blocked(rows):
+    # a [n / rows][chunk][rows][64 B] layout: per chunk, every block of `rows` rows as one
+    # contiguous 64 rows-byte piece
+    v = q.view(a.users // rows, T // 64, rows * 64)
+
+    def f(r=0):
+        for c in range(T // 64):
+            v[:, c].fill_(r & 255)
+    return f
+
+
 res = {"users": a.users, "tile": T, "dim": a.dim,
-       "with_q_ms": timed(with_q), "gb_only_ms": timed(gb_only), "fill_q_ms": timed(fill)}
+       "fill_blk16_ms": timed(blocked(16)), "fill_blk64_ms": timed(blocked(64)),
+       "with_q_ms": timed(with_q), "gb_only_ms": timed(gb_only), "fill_q_ms": timed(fill),
+       "fill_64B_pieces_ms": timed(strided(64)), "fill_128B_pieces_ms": timed(strided(128)),
+       "fill_256B_pieces_ms": timed(strided(256))}
 with_q(0)  # bitwise fingerprint of one tile's bounds (A/B builds must agree)
 torch.cuda.synchronize()
 res["q_sum"] = int(q.to(torch.int64).sum())
