@@ -314,6 +314,20 @@ def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512,
 # bound of lg_score_chunk_bound.
 SCREEN_MARGIN = 0.0081
 SCREEN_DEFAULT = True  # measured: 26.8 vs 31.9 ms (d=64), 45.8 vs 59.7 ms (d=128) at C5
+# The screened kernel's fixed costs (bf16 operands, margins, seed pass) lose to the plain
+# kernel below these user x item counts (profiles/r06_topk_guard.log, d = 64, 22 shapes from
+# 1024 x 2000 to 2048 x 1M: at k = 20 the two meet near 6e8 -- 2048 x 300K 1.39 vs 1.41 ms --,
+# the screen loses at 512 x 1M and wins at 4096 x 200K; at k = 100 near 1e9 -- it loses at
+# 8192 x 100K and 16384 x 50K, wins at 32768 x 30K and 2048 x 1M)
+SCREEN_MIN_WORK = {32: 6e8, 128: 1e9}  # k <= key -> least users x items for the screen
+
+
+def screen_pays(n_users: int, n_items: int, k: int) -> bool:
+    """Whether the default top-K dispatch takes the screened kernel for this shape."""
+    for kmax, work in SCREEN_MIN_WORK.items():
+        if k <= kmax:
+            return float(n_users) * float(n_items) >= work
+    return False  # (k > 128: the screened kernel does not take it)
 
 
 def screen_margins(un: torch.Tensor, ue: torch.Tensor, inorm: torch.Tensor,
@@ -349,12 +363,12 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
     indices int64 [U,k]) sorted by (score desc, item asc). screen=True runs
     lg_score_topk_screened_f32: a bf16 MFMA bound decides which 16-item tiles get the exact
     fp32 chain; the results are lg_score_topk_f32's (screen=False) bit for bit. Default:
-    SCREEN_DEFAULT."""
-    if screen is None:
-        screen = SCREEN_DEFAULT
+    SCREEN_DEFAULT where it pays for the shape (screen_pays)."""
     eu, ei = _f32(eu, "eu"), _f32(ei, "ei")
     nu, d = eu.shape
     ni = ei.shape[0]
+    if screen is None:
+        screen = SCREEN_DEFAULT and screen_pays(nu, ni, k)
     if ei.shape[1] != d:
         raise ValueError("eu/ei dims differ")
     if excl is not None and excl.n_rows != nu:

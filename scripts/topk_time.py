@@ -21,6 +21,7 @@ ap.add_argument("--splits", default="auto,1")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--users", type=int, default=32768)
 ap.add_argument("--k", type=int, default=20)
+ap.add_argument("--items", type=int, default=1_000_000)
 ap.add_argument("--no-excl", action="store_true", help="no exclusion sets")
 args = ap.parse_args()
 import ctypes  # noqa: E402
@@ -33,7 +34,7 @@ if counts is not None:
     counts(_buf)
 
 dev = torch.device("cuda:0")
-U, I, k = args.users, 1_000_000, args.k
+U, I, k = args.users, args.items, args.k
 for D in [int(x) for x in args.dims.split(",")]:
     g = torch.Generator(device=dev).manual_seed(42)
     eu = torch.randn(U, D, device=dev, generator=g) * 0.1

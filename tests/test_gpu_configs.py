@@ -162,7 +162,7 @@ def test_c5_forward_sampled_rows_d128(c5):
 
 @pytest.mark.parametrize("k", [20, 100])
 def test_c5_topk_512_users_vs_reference_ops(c5, k):
-    """The screened top-K (the product default) over all 1M items for 512 users (train|val =
+    """The product top-K dispatch (ops.score_topk's default) over all 1M items for 512 users (train|val =
     every interaction masked) against torch.matmul + -1024 index-put + torch.topk on the
     host, at k = 20 and at the reference's production k = 100 (const.py:433)."""
     from lgcnhs import ops

@@ -238,7 +238,7 @@ def test_score_topk_large_catalog_sample(d, k):
     eu, ei = _emb(U, d, 7), _emb(I, d, 8)
     rp, col = _excl(U, I, 1e-4, 9)
     ov, oi = O.chain_topk(eu.numpy(), ei.numpy(), rp, col, k)
-    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I))
+    v, i = ops.score_topk(eu.to(DEV), ei.to(DEV), k, _rowsets(rp, col, U, I), screen=True)
     np.testing.assert_array_equal(i.cpu().numpy(), oi)
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 

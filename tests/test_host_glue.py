@@ -72,3 +72,17 @@ def test_saved_recs_sidecar_follows_its_npy(tmp_path):
     os.utime(path, (t + 10, t + 10))  # the .npy rewritten after its sidecar
     with pytest.raises(CACHE_ERRORS):
         load_recs(path)
+
+
+def test_topk_dispatch_guard_follows_the_measured_crossover():
+    """ops.screen_pays: the default top-K takes the screened kernel only where it measured
+    faster than the plain one (profiles/r06_topk_guard.log) -- the C5 bench shape and the
+    2-rank rehearsal shape screen, few-user or small-catalog calls do not."""
+    from lgcnhs import ops
+    assert ops.screen_pays(32768, 1_000_000, 20) and ops.screen_pays(32768, 1_000_000, 100)
+    assert ops.screen_pays(8192, 200_000, 20) and ops.screen_pays(8192, 200_000, 100)
+    assert ops.screen_pays(2048, 1_000_000, 100)
+    assert not ops.screen_pays(512, 1_000_000, 20)
+    assert not ops.screen_pays(8192, 30_000, 20)
+    assert not ops.screen_pays(8192, 100_000, 100)
+    assert not ops.screen_pays(1, 10**9, 129)  # (beyond the screened kernel's k)
