@@ -1378,7 +1378,9 @@ struct UState {
   int32_t xw;
 };
 
-template <int MODE, int D, int M>
+// SEED: the first tile's instance (lists start empty): the finish scores the columns with the
+// largest bounds first (below); a separate instance so the other tiles' code is untouched
+template <int MODE, int D, int M, bool SEED = false>
 __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
   constexpr int Q = kWalkQ;
   extern __shared__ double lds[];
@@ -1831,6 +1833,110 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
         sc_v = s_rbc[lane < a.nch ? lane : 0] * (1.0 + 0x1p-50) * gp * (1.0 / 255.0);
         bq_v = gp * (1.0 / 255.0) * (1.0 + 0x1p-50);
       }
+      // Seeding (the first tile's instance; G, k <= 64, a list that is not full): with tau = -inf
+      // every column would pass and be scored exactly until the list fills and tau climbs from
+      // whatever the first columns scored. Instead the columns whose pre-screen bound
+      // b = acc q sc is at least t_hi = the k-th largest of the lanes' maximum bounds (so at
+      // least k columns) are scored first (pass A), tau starts at the k-th best of them, and
+      // the scan below skips exactly those columns (the same b, computed the same way). The
+      // candidate set and the list order are unchanged, so the list is the same.
+      bool seeded = false;
+      double t_hi = 0.0;
+      if constexpr (SEED && D > 0 && !kTwo) {  // (kTwo: k > 64, two list registers per lane)
+        if (tau == neg_inf<double>()) {
+          // step s8's columns c0 = 512 s8 + ...: the 8 accumulator values of the lane (read
+          // only; the scan below zeroes them) and their bounds b, computed as the scan does
+          auto read8 = [&](int c0, double (&sv)[8]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+              for (int pp = 0; pp < 2; ++pp) {
+                const int j = c0 + 256 * hh + 4 * lane + 2 * pp;
+                const double2 x = *reinterpret_cast<const double2 *>(acc + j);
+                sv[4 * hh + 2 * pp] = x.x;
+                sv[4 * hh + 2 * pp + 1] = x.y;
+              }
+            if (c0 + 512 > a.width) {
+#pragma unroll
+              for (int t = 0; t < 8; ++t) {
+                const int j = c0 + 256 * (t >> 2) + 4 * lane + (t & 3);
+                if (j >= a.width) sv[t] = neg_inf<double>();
+              }
+            }
+          };
+          auto qsel = [&](int i) __attribute__((always_inline)) {  // qr[i] for a uniform i
+            uint32_t v = 0xFFFFFFFFu;  // (columns past 256 kQPre: the chunk bound alone)
+#pragma unroll
+            for (int x = 0; x < kQPre; ++x) v = i == x ? qr[x] : v;
+            return v;
+          };
+          auto bound = [&](int c0, int t, double svt, uint32_t qa, uint32_t qb2)
+              __attribute__((always_inline)) {
+            const double sc = __shfl(sc_v, ((c0 + 256 * (t >> 2) + 4 * lane) >> 6) & 63);
+            const uint32_t qq = t < 4 ? qa : qb2;
+            const double qv = (double)((qq >> (8 * (t & 3))) & 0xFFu);
+            return svt * qv * sc;
+          };
+          double lmax = neg_inf<double>();
+#pragma unroll 1
+          for (int c0 = 0; c0 < a.width; c0 += 512) {
+            double sv[8];
+            read8(c0, sv);
+            const uint32_t qa = qsel(c0 >> 8), qb2 = qsel((c0 >> 8) + 1);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const double bt = bound(c0, t, sv[t], qa, qb2);
+              lmax = bt > lmax ? bt : lmax;  // (NaN: skipped)
+            }
+          }
+          // the k-th largest lane maximum: bitonic sort of the 64 values, descending
+          double v = lmax;
+#pragma unroll
+          for (int sz = 2; sz <= 64; sz <<= 1)
+#pragma unroll
+            for (int st2 = sz >> 1; st2 > 0; st2 >>= 1) {
+              const double o = __shfl_xor(v, st2);
+              const bool keep_max = ((lane & sz) == 0) == ((lane & st2) == 0);
+              v = keep_max ? (o > v ? o : v) : (o < v ? o : v);
+            }
+          t_hi = __shfl(v, k - 1);
+          seeded = true;
+          // pass A: score every column with b >= t_hi (16 at a time), insert
+#pragma unroll 1
+          for (int c0 = 0; c0 < a.width; c0 += 512) {
+            double sv[8];
+            read8(c0, sv);
+            const uint32_t qa = qsel(c0 >> 8), qb2 = qsel((c0 >> 8) + 1);
+            uint32_t mask = 0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {  // (excluded columns: b = -inf or NaN, never taken)
+              const double bt = bound(c0, t, sv[t], qa, qb2);
+              mask |= bt >= t_hi && bt > neg_inf<double>() ? 1u << t : 0u;
+            }
+            while (__ballot(mask != 0)) {
+              const bool has = mask != 0;
+              const int t = has ? __ffs(mask) - 1 : 0;
+              mask &= mask - 1;
+              double sx = sv[0];
+#pragma unroll
+              for (int x = 1; x < 8; ++x) sx = t == x ? sv[x] : sx;
+              const int j = c0 + 256 * (t >> 2) + 4 * lane + (t & 3);
+              const double f = has ? sx * s_rb[has ? j : 0] : -1.0;
+              const uint64_t bal = __ballot(has);
+              const int nb = __popcll(bal);
+              if (ncand + nb > kOvfList) flush();
+              if (has) {
+                const int p = ncand + __popcll(bal & lanemask_lt());
+                cq_f[p] = f;
+                cq_j[p] = (uint32_t)j;
+              }
+              ncand += nb;
+              if (ncand >= 16) flush();
+            }
+          }
+          if (ncand) flush();
+        }
+      }
       const double2 zero2{0.0, 0.0};
       for (int c0 = 0; c0 < a.width; c0 += 512) {
         const uint32_t qa = qr[0], qb2 = qr[1];
@@ -1869,7 +1975,9 @@ __global__ __launch_bounds__(512) void k_tile_walk(WalkArgs a) {
           if constexpr (D > 0) {
             const uint32_t qq = t < 4 ? qa : qb2;
             const double qv = (double)((qq >> (8 * (t & 3))) & 0xFFu);
-            pre = sv[t] * qv * (t < 4 ? sc0 : sc1) > tau;
+            const double b = sv[t] * qv * (t < 4 ? sc0 : sc1);
+            // (seeded: pass A scored the columns with b >= t_hi, b > -inf)
+            pre = b > tau && !(seeded && b >= t_hi && b > neg_inf<double>());
           } else {
             pre = sv[t] > thr_s;
           }
@@ -2337,7 +2445,14 @@ static int launch_walk(const WalkArgs &a, hipStream_t s) {
   const int64_t cap = n_cus();
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   const size_t lds = shared + (size_t)nw * per;
-  k_tile_walk<MODE, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
+  bool seeded = false;
+  if constexpr (D > 0 && M <= 2) {  // (the seeded finish: k <= 64 with a G factor)
+    if (a.first) {
+      k_tile_walk<MODE, D, M, true><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
+      seeded = true;
+    }
+  }
+  if (!seeded) k_tile_walk<MODE, D, M><<<dim3(blocks), dim3(64 * nw), lds, s>>>(a);
   return LG_OK;
 }
 
