@@ -210,10 +210,11 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 #define LG_BOUND_NB(D) ((D) <= 64 ? 5 : 4)
 #endif
 
-// cache-policy bits of the q and gb stores: nt (streaming; 0.84 -> 0.75 ms per C5 tile for
-// the q stores, scripts/micro_bound.py)
+// cache-policy bits of the q and gb stores (measurement builds): nt on the q stores measured
+// 0.84 -> 0.75 ms per C5 tile alone (scripts/micro_bound.py) but 0.728 -> 0.778 ms inside the
+// LGCNHS pipeline (scripts/gpu_r06_qab.sh), so the default is plain stores
 #ifndef LG_QSTORE_AUX
-#define LG_QSTORE_AUX 2
+#define LG_QSTORE_AUX 0
 #endif
 #ifndef LG_GB_AUX
 #define LG_GB_AUX 0
