@@ -184,13 +184,6 @@ __global__ __launch_bounds__(256) void k_bound_prep4(const float *__restrict__ x
   }
 }
 
-// One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile; a block = 4
-// waves = 256 users. The chunk's item fragments (64 items x D bf16) are shared by the block's
-// waves through LDS: the 256 threads load chunk c + 1 into registers while chunk c is computed
-// from its LDS buffer, store it into the other buffer afterwards, and one barrier per chunk
-// hands it over -- a quarter of the L2 fragment reads, and their latency hidden by a whole
-// chunk of work. W = waves per SIMD the registers and LDS are sized for (D <= 64: 3, D = 128:
-// 2). Waves past the last user still load and synchronise (their stores are masked).
 // s_waitcnt vmcnt(n) for a uniform run-time n <= K (the count is an immediate: a chain of
 // scalar compares picks the instruction)
 template <int K>
@@ -219,6 +212,13 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 #ifndef LG_GB_AUX
 #define LG_GB_AUX 0
 #endif
+// One wave = 64 users (4 groups of 16 MFMA columns) x every chunk of the tile; a block = 4
+// waves = 256 users. The chunk's item fragments (64 items x D bf16) are shared by the block's
+// waves through LDS: an NB-buffer ring filled by LDS-DMA NB - 1 chunks ahead, one barrier per
+// chunk hands a buffer over -- a quarter of the L2 fragment reads, their latency hidden by
+// NB - 2 chunks of work. W = waves per SIMD the registers are sized for (D <= 64: 3, D = 128:
+// 2). Waves past the last user still load and synchronise (their stores are dropped by the
+// descriptors' range checks).
 template <int D, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void k_chunk_bound(const __bf16 *__restrict__ ub,
                                                      const float *__restrict__ unorm,
