@@ -1525,6 +1525,12 @@ __global__ __launch_bounds__(256) void k_seed_combine(const float *__restrict__ 
 #ifndef LG_SEED4_LA
 #define LG_SEED4_LA 5
 #endif
+// one user group per wave for the 4-slab GL shape at d <= 64 (k > 64: 128 users per block,
+// one split at C5): k = 100 16.9 -> 16.1 ms, k = 128 18.8 -> 17.6 ms; k = 50 / 64 keep 2 groups
+// (13.1 / 14.9 ms with 1 against 12.4 / 14.6; scripts/gpu_r06_glng.sh)
+#ifndef LG_GL4_NG
+#define LG_GL4_NG 1
+#endif
 #ifndef LG_GL_NG  // user groups per wave in the GL shapes (4: 512 users per block)
 #define LG_GL_NG 2
 #endif
@@ -1564,7 +1570,8 @@ static void dispatch_topk_screen(int M, bool seedp, const float *eu, const float
   if (gm == 2) {
     LG_RING_LAUNCH(LG_GL_NG, 8, 2, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
   } else if (gm == 4) {
-    LG_RING_LAUNCH(LG_GL_NG, 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1, false, true)
+    LG_RING_LAUNCH((D <= 64 ? LG_GL4_NG : LG_GL_NG), 8, 4, LG_GL_CAP, LG_GL_NBUF, LG_GL_LA, 1,
+                   false, true)
   } else if (M == 1 && seedp) {
     LG_RING_LAUNCH(LG_RING_NG, LG_RING_W, 1, LG_RING_CAP, LG_RING_NBUF, LG_RING_LA,
                    LG_RING_LAG, true, false)

@@ -282,22 +282,22 @@ def _resident_blocks(device, k: int = 64, screen: bool = False) -> int:
     return per_cu * torch.cuda.get_device_properties(device).multi_processor_count
 
 
-def _users_per_block(k: int, screen: bool = False) -> int:
+def _users_per_block(k: int, screen: bool = False, d: int = 64) -> int:
     """Users per workgroup of csrc/topk.hip's launches (dispatch_topk / _screen)."""
-    if screen:  # (k > 32: the global-list shape, 8 waves x 2 groups)
-        return 256
+    if screen:  # (8 waves x 2 groups; k > 64 at d <= 64: 1 group, LG_GL4_NG)
+        return 128 if k > 64 and d <= 64 else 256
     return 128 if k <= 32 else (64 if k <= 64 else 32)
 
 
 def _splits_for(n_users: int, n_items: int, k: int, resident: int = 512,
-                screen: bool = False) -> int:
+                screen: bool = False, d: int = 64) -> int:
     """Item-range splits for lg_score_topk_f32: the fewest splits that keep every CU busy.
 
     Each split restarts every user's candidate list from an empty threshold (the warm-up
     inserts ~k*ln(items/k) candidates), so more splits cost work; too few leave CUs idle
     in the last round of workgroups. Minimise rounds/splits (the makespan in units of one
     unsplit block) with a 2 % penalty per split."""
-    per_block = _users_per_block(k, screen)
+    per_block = _users_per_block(k, screen, d)
     tiles = (n_users + per_block - 1) // per_block
     best, best_cost = 1, None
     for s in range(1, min(64, max(1, n_items // 256)) + 1):
@@ -373,7 +373,7 @@ def score_topk(eu: torch.Tensor, ei: torch.Tensor, k: int, excl: RowSets | None 
         raise ValueError("eu/ei dims differ")
     if excl is not None and excl.n_rows != nu:
         raise ValueError(f"exclusion rows {excl.n_rows} != users {nu}")
-    ns = (_splits_for(nu, ni, k, _resident_blocks(eu.device, k, screen), screen)
+    ns = (_splits_for(nu, ni, k, _resident_blocks(eu.device, k, screen), screen, d)
           if n_splits is None else int(n_splits))
     ws_fn = (N.lib().lg_score_topk_screened_ws_bytes if screen and nu > 0
              else N.lib().lg_score_topk_ws_bytes)
